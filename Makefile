@@ -1,0 +1,38 @@
+# Build of the MI355X BFS engine.  Everything compiles for gfx950 only.
+#   libbfsx.so   : C-ABI (include/bfsx.h) + HIP kernels   -> bfs-with-mapreduce_amd/libbfsx.so
+#   bfsx_spark   : C++ host twin of BfsSpark.main          -> bfs-with-mapreduce_amd/bfsx_spark
+#   liboracle.so : CPU oracle (test infrastructure only)   -> oracle/liboracle.so
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+PKG      := bfs-with-mapreduce_amd
+CSRC     := $(PKG)/csrc
+HOSTSRC  := $(PKG)/host
+OBJDIR   := $(PKG)/build
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result -I include
+CXXFLAGS ?= -O2 -std=c++17 -Wall -I include
+
+KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip
+HOST_SRCS   := $(CSRC)/bfsx_api.cpp
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
+
+all: $(PKG)/libbfsx.so oracle
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/bfsx_internal.h include/bfsx.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h include/bfsx.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/libbfsx.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(OBJDIR) $(PKG)/libbfsx.so $(PKG)/bfsx_spark
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,257 @@
+"""Thin ctypes binding of libbfsx.so (include/bfsx.h) used by tests, bench.py and smoke().
+
+This is plumbing, not a fallback: every compute call goes to the HIP library, and loading fails
+loudly when libbfsx.so is missing.  The reference-shaped host (BfsSpark / GraphFileUtil / Vertex /
+Color / ServiceConfiguration) is the C++ twin in host/ (bfsx_spark); this module mirrors the C-ABI
+one-to-one.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libbfsx.so")
+
+BFSX_OK = 0
+BFSX_E_IO = -1
+BFSX_E_PARSE = -2
+BFSX_E_RANGE = -3
+BFSX_E_HIP = -4
+BFSX_E_RCCL = -5
+BFSX_E_OOM = -6
+BFSX_E_ARG = -7
+BFSX_E_NODEV = -8
+
+DIR_AUTO, DIR_TOPDOWN, DIR_BOTTOMUP = 0, 1, 2
+INF = 2147483647
+
+# Every symbol include/bfsx.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "bfsx_abi_version", "bfsx_last_error", "bfsx_init", "bfsx_finalize", "bfsx_set_option",
+    "bfsx_parse_algs4", "bfsx_free_host", "bfsx_graph_load_algs4", "bfsx_graph_from_edges",
+    "bfsx_graph_kronecker", "bfsx_kronecker_edges", "bfsx_graph_free", "bfsx_graph_nv",
+    "bfsx_graph_nnz", "bfsx_graph_m", "bfsx_graph_csr", "bfsx_sample_roots", "bfsx_bfs",
+    "bfsx_result", "bfsx_level_times", "bfsx_level_dirs", "bfsx_level_stats",
+    "bfsx_device_synchronize",
+]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("levels", C.c_int32), ("topdown_levels", C.c_int32), ("bottomup_levels", C.c_int32),
+        ("reserved0", C.c_int32), ("reached", C.c_int64), ("m_comp", C.c_int64),
+        ("edges_examined", C.c_int64), ("t_bfs_ms", C.c_double), ("t_total_ms", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
+
+
+class LevelStat(C.Structure):
+    _fields_ = [
+        ("direction", C.c_int32), ("level", C.c_int32), ("frontier_in", C.c_int64),
+        ("frontier_out", C.c_int64), ("mf_in", C.c_int64), ("unvisited_in", C.c_int64),
+        ("scanned", C.c_int64), ("kernel_ms", C.c_double), ("cum_ms", C.c_double),
+    ]
+
+
+class BfsxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"bfsx error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_VP = C.c_void_p
+_U32PP = C.POINTER(C.POINTER(C.c_uint32))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.bfsx_last_error.restype = C.c_char_p
+        L.bfsx_init.argtypes = [C.c_int, C.POINTER(_VP)]
+        L.bfsx_finalize.argtypes = [_VP]
+        L.bfsx_finalize.restype = None
+        L.bfsx_set_option.argtypes = [_VP, C.c_char_p, C.c_char_p]
+        L.bfsx_parse_algs4.argtypes = [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _U32PP, _U32PP]
+        L.bfsx_free_host.argtypes = [_VP]
+        L.bfsx_free_host.restype = None
+        L.bfsx_graph_load_algs4.argtypes = [_VP, C.c_char_p, C.POINTER(_VP)]
+        L.bfsx_graph_from_edges.argtypes = [_VP, C.c_int64, _VP, _VP, C.c_int64, C.POINTER(_VP)]
+        L.bfsx_graph_kronecker.argtypes = [_VP, C.c_int, C.c_int, C.c_uint64, C.POINTER(_VP)]
+        L.bfsx_kronecker_edges.argtypes = [_VP, C.c_int, C.c_int, C.c_uint64, _VP, _VP]
+        L.bfsx_graph_free.argtypes = [_VP]
+        L.bfsx_graph_free.restype = None
+        for f in ("bfsx_graph_nv", "bfsx_graph_nnz", "bfsx_graph_m"):
+            getattr(L, f).argtypes = [_VP]
+            getattr(L, f).restype = C.c_int64
+        L.bfsx_graph_csr.argtypes = [_VP, _VP, _VP]
+        L.bfsx_sample_roots.argtypes = [_VP, C.c_int, C.c_uint64, _VP]
+        L.bfsx_bfs.argtypes = [_VP, C.c_int64, _VP, _VP, C.POINTER(Stats)]
+        L.bfsx_result.argtypes = [_VP, _VP, _VP]
+        L.bfsx_level_times.argtypes = [_VP, _VP, C.c_int]
+        L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
+        L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
+        L.bfsx_device_synchronize.argtypes = [_VP]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != BFSX_OK:
+        raise BfsxError(rc, lib().bfsx_last_error().decode(errors="replace"))
+    return rc
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def parse_algs4(path):
+    """GraphFileUtil.convert parse (host only, no GPU needed) -> (nv, u, v)."""
+    nv, m = C.c_int64(), C.c_int64()
+    up, vp = C.POINTER(C.c_uint32)(), C.POINTER(C.c_uint32)()
+    _check(lib().bfsx_parse_algs4(os.fsencode(path), C.byref(nv), C.byref(m), C.byref(up), C.byref(vp)))
+    try:
+        n = m.value
+        u = np.ctypeslib.as_array(up, shape=(max(n, 1),))[:n].copy()
+        v = np.ctypeslib.as_array(vp, shape=(max(n, 1),))[:n].copy()
+    finally:
+        lib().bfsx_free_host(up)
+        lib().bfsx_free_host(vp)
+    return nv.value, u, v
+
+
+class Context:
+    """One device (bfsx_init .. bfsx_finalize)."""
+
+    def __init__(self, device=0, **options):
+        h = _VP()
+        _check(lib().bfsx_init(device, C.byref(h)))
+        self._h = h
+        for k, val in options.items():
+            self.set_option(k, val)
+
+    def set_option(self, key, value):
+        _check(lib().bfsx_set_option(self._h, key.encode(), str(value).encode()))
+
+    def load_algs4(self, path):
+        g = _VP()
+        _check(lib().bfsx_graph_load_algs4(self._h, os.fsencode(path), C.byref(g)))
+        return Graph(self, g)
+
+    def from_edges(self, nv, u, v):
+        u = np.ascontiguousarray(u, dtype=np.uint32)
+        v = np.ascontiguousarray(v, dtype=np.uint32)
+        g = _VP()
+        _check(lib().bfsx_graph_from_edges(self._h, nv, _p(u), _p(v), len(u), C.byref(g)))
+        return Graph(self, g)
+
+    def kronecker(self, scale, edgefactor=16, seed=0x5EED2026):
+        g = _VP()
+        _check(lib().bfsx_graph_kronecker(self._h, scale, edgefactor, seed, C.byref(g)))
+        return Graph(self, g)
+
+    def kronecker_edges(self, scale, edgefactor=16, seed=0x5EED2026):
+        m = edgefactor << scale
+        u = np.empty(m, np.uint32)
+        v = np.empty(m, np.uint32)
+        _check(lib().bfsx_kronecker_edges(self._h, scale, edgefactor, seed, _p(u), _p(v)))
+        return u, v
+
+    def synchronize(self):
+        _check(lib().bfsx_device_synchronize(self._h))
+
+    def close(self):
+        if self._h:
+            lib().bfsx_finalize(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class Graph:
+    def __init__(self, ctx, handle):
+        self.ctx = ctx
+        self._h = handle
+
+    @property
+    def nv(self):
+        return lib().bfsx_graph_nv(self._h)
+
+    @property
+    def nnz(self):
+        return lib().bfsx_graph_nnz(self._h)
+
+    @property
+    def m(self):
+        return lib().bfsx_graph_m(self._h)
+
+    def csr(self):
+        off = np.empty(self.nv + 1, np.int64)
+        col = np.empty(max(self.nnz, 1), np.uint32)
+        _check(lib().bfsx_graph_csr(self._h, _p(off), _p(col)))
+        return off, col[: self.nnz]
+
+    def sample_roots(self, count, seed=0x5EED):
+        r = np.empty(count, np.int64)
+        _check(lib().bfsx_sample_roots(self._h, count, seed, _p(r)))
+        return r
+
+    def bfs(self, source, want_dist=True, want_parent=True):
+        """Returns (dist int32[nv] or None, parent int64[nv] or None, stats dict)."""
+        nv = self.nv
+        dist = np.empty(nv, np.int32) if want_dist else None
+        parent = np.empty(nv, np.int64) if want_parent else None
+        st = Stats()
+        _check(lib().bfsx_bfs(self._h, source, _p(dist), _p(parent), C.byref(st)))
+        return dist, parent, st.as_dict()
+
+    def bfs_device_only(self, source):
+        """The timed hot path: results stay on the device, no stats reduction.
+        Returns the device time (ms) of source init -> last level (hipEvents)."""
+        _check(lib().bfsx_bfs(self._h, source, None, None, None))
+        buf = np.empty(1 << 16, np.float64)
+        n = lib().bfsx_level_times(self._h, _p(buf), len(buf))
+        return float(buf[n - 1]) if n > 0 else float("nan")
+
+    def result(self):
+        dist = np.empty(self.nv, np.int32)
+        parent = np.empty(self.nv, np.int64)
+        _check(lib().bfsx_result(self._h, _p(dist), _p(parent)))
+        return dist, parent
+
+    def level_times(self, cap=1 << 20):
+        buf = np.empty(cap, np.float64)
+        n = lib().bfsx_level_times(self._h, _p(buf), cap)
+        return buf[:n].copy()
+
+    def level_dirs(self, cap=1 << 20):
+        buf = np.empty(cap, np.int32)
+        n = lib().bfsx_level_dirs(self._h, _p(buf), cap)
+        return buf[:n].copy()
+
+    def level_stats(self, cap=1 << 16):
+        buf = (LevelStat * cap)()
+        n = lib().bfsx_level_stats(self._h, buf, cap)
+        return [{k: getattr(buf[i], k) for k, _ in LevelStat._fields_} for i in range(n)]
+
+    def free(self):
+        if self._h:
+            lib().bfsx_graph_free(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.free()

@@ -1,0 +1,437 @@
+// bfsx_api.cpp -- the C-ABI of libbfsx.so (declared in include/bfsx.h).
+//
+// Host side of the drop-in boundary: error plumbing, the algs4 edge-list parser with
+// GraphFileUtil.convert semantics (GraphFileUtil.java:45-66), graph handles, root sampling and the
+// synchronous bfsx_bfs wrapper around the device level loop (kernels_bfs.hip).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_set>
+
+#include "bfsx_internal.h"
+
+namespace bfsx {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+namespace {
+
+inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// Integer.parseInt over an exact token: optional sign, >= 1 ASCII digit, int32 range, no trimming.
+inline bool parse_java_int(const char *s, size_t n, int64_t &out) {
+    if (n == 0) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') {
+        neg = s[0] == '-';
+        if (n == 1) return false;
+        i = 1;
+    }
+    int64_t val = 0;
+    for (; i < n; i++) {
+        const unsigned d = (unsigned)(s[i] - '0');
+        if (d > 9) return false;
+        val = val * 10 + d;
+        if (val > 2147483648LL) return false;
+    }
+    if (neg) val = -val;
+    if (val > 2147483647LL) return false;
+    out = val;
+    return true;
+}
+
+struct MappedFile {
+    const char *p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    ~MappedFile() {
+        if (p && n) munmap((void *)p, n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+// BufferedReader.readLine line splitting: '\n', '\r' or "\r\n" end a line; no trailing empty line.
+struct LineReader {
+    const char *b;
+    size_t n, pos = 0;
+    bool next(const char *&ls, size_t &ll) {
+        if (pos >= n) return false;
+        const size_t s = pos;
+        const void *nl = memchr(b + s, '\n', n - s);
+        size_t e = nl ? (size_t)((const char *)nl - b) : n;
+        const void *cr = memchr(b + s, '\r', e - s);
+        if (cr) e = (size_t)((const char *)cr - b);
+        ls = b + s;
+        ll = e - s;
+        if (e < n) e += (b[e] == '\r' && e + 1 < n && b[e + 1] == '\n') ? 2 : 1;
+        pos = e;
+        return true;
+    }
+};
+
+template <class T>
+struct HostVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    ~HostVec() { free(p); }
+    bool push(T x) {
+        if (n == cap) {
+            size_t nc = cap ? cap * 2 : 4096;
+            T *q = (T *)realloc(p, nc * sizeof(T));
+            if (!q) return false;
+            p = q;
+            cap = nc;
+        }
+        p[n++] = x;
+        return true;
+    }
+    T *release() {
+        T *q = p;
+        p = nullptr;
+        return q;
+    }
+};
+
+} // namespace
+} // namespace bfsx
+
+using namespace bfsx;
+
+extern "C" {
+
+int bfsx_abi_version(void) { return BFSX_ABI_VERSION; }
+
+const char *bfsx_last_error(void) { return g_last_error.c_str(); }
+
+void bfsx_free_host(void *p) { free(p); }
+
+int bfsx_parse_algs4(const char *path, int64_t *nv_out, int64_t *m_out, uint32_t **u_out, uint32_t **v_out) {
+    if (!path || !nv_out || !m_out || !u_out || !v_out) return fail(BFSX_E_ARG, "null argument");
+    MappedFile f;
+    f.fd = open(path, O_RDONLY);
+    if (f.fd < 0) return fail(BFSX_E_IO, std::string("cannot open ") + path + ": " + strerror(errno));
+    struct stat sb;
+    if (fstat(f.fd, &sb) != 0) return fail(BFSX_E_IO, std::string("cannot stat ") + path);
+    f.n = (size_t)sb.st_size;
+    if (f.n) {
+        void *m = mmap(nullptr, f.n, PROT_READ, MAP_PRIVATE, f.fd, 0);
+        if (m == MAP_FAILED) return fail(BFSX_E_IO, std::string("cannot map ") + path);
+        f.p = (const char *)m;
+        madvise(m, f.n, MADV_SEQUENTIAL);
+    }
+    LineReader lr{f.p, f.n};
+    const char *ls;
+    size_t ll;
+    // GraphFileUtil.java:48  int vertexCount = Integer.parseInt(reader.readLine());
+    if (!lr.next(ls, ll)) return fail(BFSX_E_PARSE, "missing vertex count line (parseInt(null))");
+    int64_t V;
+    if (!parse_java_int(ls, ll, V)) return fail(BFSX_E_PARSE, "line 1: vertex count is not an int");
+    if (V < 0) return fail(BFSX_E_PARSE, "line 1: negative vertex count (HashMap capacity)");
+    const int64_t nv = V > 0 ? V : 1; // vertex 0 is always created (GraphFileUtil.java:53)
+    lr.next(ls, ll);                  // GraphFileUtil.java:58-59: edge count, unused
+    HostVec<uint32_t> us, vs;
+    int64_t lineno = 2;
+    while (lr.next(ls, ll)) { // GraphFileUtil.java:60-66, to EOF
+        lineno++;
+        const char *sp = (const char *)memchr(ls, ' ', ll);
+        if (!sp) return fail(BFSX_E_PARSE, "line " + std::to_string(lineno) + ": expected two tokens");
+        const size_t n0 = (size_t)(sp - ls);
+        const char *t1 = sp + 1;
+        const char *sp2 = (const char *)memchr(t1, ' ', ll - n0 - 1);
+        const size_t n1 = sp2 ? (size_t)(sp2 - t1) : ll - n0 - 1;
+        int64_t a, b;
+        if (!parse_java_int(ls, n0, a) || !parse_java_int(t1, n1, b))
+            return fail(BFSX_E_PARSE, "line " + std::to_string(lineno) + ": token is not an int");
+        if (a < 0 || a >= nv || b < 0 || b >= nv)
+            return fail(BFSX_E_RANGE, "line " + std::to_string(lineno) + ": vertex id outside [0," +
+                                          std::to_string(nv) + ")");
+        if (!us.push((uint32_t)a) || !vs.push((uint32_t)b)) return fail(BFSX_E_OOM, "out of host memory");
+    }
+    *nv_out = nv;
+    *m_out = (int64_t)us.n;
+    *u_out = us.release();
+    *v_out = vs.release();
+    if (!*u_out) *u_out = (uint32_t *)malloc(sizeof(uint32_t));
+    if (!*v_out) *v_out = (uint32_t *)malloc(sizeof(uint32_t));
+    return BFSX_OK;
+}
+
+int bfsx_init(int device, bfsx_ctx **out) {
+    if (!out) return fail(BFSX_E_ARG, "null out");
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) return fail(BFSX_E_NODEV, "no HIP device available");
+    if (device < 0 || device >= count) return fail(BFSX_E_ARG, "device ordinal out of range");
+    BFSX_HIP_TRY(hipSetDevice(device));
+    auto *ctx = new (std::nothrow) bfsx_ctx();
+    if (!ctx) return fail(BFSX_E_OOM, "ctx");
+    ctx->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
+    if (ctx->num_cus <= 0) ctx->num_cus = 256;
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(BFSX_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    *out = ctx;
+    return BFSX_OK;
+}
+
+void bfsx_finalize(bfsx_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
+    if (!ctx || !key || !value) return fail(BFSX_E_ARG, "null argument");
+    const std::string k(key), v(value);
+    auto as_int = [&](int &dst) -> int {
+        char *end = nullptr;
+        long x = strtol(value, &end, 10);
+        if (!end || *end || x <= 0 || x > (1L << 30)) return fail(BFSX_E_ARG, "bad integer for " + k);
+        dst = (int)x;
+        return BFSX_OK;
+    };
+    if (k == "direction") {
+        if (v == "auto") ctx->opt.direction = BFSX_DIR_AUTO;
+        else if (v == "topdown") ctx->opt.direction = BFSX_DIR_TOPDOWN;
+        else if (v == "bottomup") ctx->opt.direction = BFSX_DIR_BOTTOMUP;
+        else return fail(BFSX_E_ARG, "direction must be auto|topdown|bottomup");
+        return BFSX_OK;
+    }
+    if (k == "alpha") return as_int(ctx->opt.alpha);
+    if (k == "beta") return as_int(ctx->opt.beta);
+    if (k == "hub_degree") {
+        int h = 0;
+        int rc = as_int(h);
+        if (!rc) ctx->opt.hub_degree = (uint32_t)h;
+        return rc;
+    }
+    return fail(BFSX_E_ARG, "unknown option " + k);
+}
+
+static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m,
+                                   bfsx_graph **out) {
+    auto *g = new (std::nothrow) bfsx_graph();
+    if (!g) return fail(BFSX_E_OOM, "graph");
+    g->ctx = ctx;
+    g->nv = nv;
+    g->m = m;
+    int rc = build_csr_device(ctx->stream, nv, d_u, d_v, m, &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt);
+    if (rc) {
+        delete g;
+        return rc;
+    }
+    *out = g;
+    return BFSX_OK;
+}
+
+int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
+                          bfsx_graph **out) {
+    if (!ctx || !out || nv <= 0 || m < 0 || (m > 0 && (!u || !v))) return fail(BFSX_E_ARG, "bad argument");
+    if (nv > (int64_t)INT32_MAX) return fail(BFSX_E_ARG, "nv must be < 2^31 on one device");
+    for (int64_t i = 0; i < m; i++)
+        if ((int64_t)u[i] >= nv || (int64_t)v[i] >= nv)
+            return fail(BFSX_E_RANGE, "tuple " + std::to_string(i) + " has a vertex id >= nv");
+    BFSX_HIP_TRY(hipSetDevice(ctx->device));
+    uint32_t *d_u = nullptr, *d_v = nullptr;
+    BFSX_HIP_TRY(hipMalloc(&d_u, std::max<int64_t>(m, 1) * sizeof(uint32_t)));
+    hipError_t e = hipMalloc(&d_v, std::max<int64_t>(m, 1) * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        (void)hipFree(d_u);
+        return fail(BFSX_E_OOM, "device tuples");
+    }
+    int rc = BFSX_OK;
+    if (m > 0) {
+        if (hipMemcpyAsync(d_u, u, m * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(d_v, v, m * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            rc = fail(BFSX_E_HIP, "H2D tuples");
+    }
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, out);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    return rc;
+}
+
+int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
+    if (!ctx || !path || !out) return fail(BFSX_E_ARG, "null argument");
+    int64_t nv = 0, m = 0;
+    uint32_t *u = nullptr, *v = nullptr;
+    int rc = bfsx_parse_algs4(path, &nv, &m, &u, &v);
+    if (rc) return rc;
+    rc = bfsx_graph_from_edges(ctx, nv, u, v, m, out);
+    free(u);
+    free(v);
+    return rc;
+}
+
+int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, uint32_t *u, uint32_t *v) {
+    if (!ctx || !u || !v || scale < 1 || scale > 31 || edgefactor < 1) return fail(BFSX_E_ARG, "bad argument");
+    BFSX_HIP_TRY(hipSetDevice(ctx->device));
+    const int64_t m = (int64_t)edgefactor << scale;
+    uint32_t *d_u = nullptr, *d_v = nullptr;
+    BFSX_HIP_TRY(hipMalloc(&d_u, m * sizeof(uint32_t)));
+    if (hipMalloc(&d_v, m * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(d_u);
+        return fail(BFSX_E_OOM, "device tuples");
+    }
+    int rc = kronecker_generate(ctx->stream, scale, edgefactor, seed, d_u, d_v);
+    if (!rc && (hipMemcpyAsync(u, d_u, m * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                hipMemcpyAsync(v, d_v, m * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                hipStreamSynchronize(ctx->stream) != hipSuccess))
+        rc = fail(BFSX_E_HIP, "D2H tuples");
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    return rc;
+}
+
+int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, bfsx_graph **out) {
+    if (!ctx || !out || scale < 1 || scale > 30 || edgefactor < 1) return fail(BFSX_E_ARG, "bad argument");
+    BFSX_HIP_TRY(hipSetDevice(ctx->device));
+    const int64_t nv = (int64_t)1 << scale;
+    const int64_t m = (int64_t)edgefactor << scale;
+    uint32_t *d_u = nullptr, *d_v = nullptr;
+    BFSX_HIP_TRY(hipMalloc(&d_u, m * sizeof(uint32_t)));
+    if (hipMalloc(&d_v, m * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(d_u);
+        return fail(BFSX_E_OOM, "device tuples");
+    }
+    int rc = kronecker_generate(ctx->stream, scale, edgefactor, seed, d_u, d_v);
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, out);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    return rc;
+}
+
+void bfsx_graph_free(bfsx_graph *g) {
+    if (!g) return;
+    (void)hipSetDevice(g->ctx->device);
+    bfs_workspace_free(g->ws);
+    if (g->d_row_off) (void)hipFree(g->d_row_off);
+    if (g->d_col) (void)hipFree(g->d_col);
+    if (g->d_tuple_cnt) (void)hipFree(g->d_tuple_cnt);
+    delete g;
+}
+
+int64_t bfsx_graph_nv(const bfsx_graph *g) { return g ? g->nv : -1; }
+int64_t bfsx_graph_nnz(const bfsx_graph *g) { return g ? g->nnz : -1; }
+int64_t bfsx_graph_m(const bfsx_graph *g) { return g ? g->m : -1; }
+
+int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col) {
+    if (!g) return fail(BFSX_E_ARG, "null graph");
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    if (row_off)
+        BFSX_HIP_TRY(hipMemcpyAsync(row_off, g->d_row_off, (g->nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                    g->ctx->stream));
+    if (col && g->nnz)
+        BFSX_HIP_TRY(
+            hipMemcpyAsync(col, g->d_col, g->nnz * sizeof(uint32_t), hipMemcpyDeviceToHost, g->ctx->stream));
+    BFSX_HIP_TRY(hipStreamSynchronize(g->ctx->stream));
+    return BFSX_OK;
+}
+
+int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
+    if (!g || !roots || count < 0) return fail(BFSX_E_ARG, "bad argument");
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    std::unordered_set<int64_t> seen;
+    int found = 0;
+    const uint64_t max_tries = 1000ull + 1000ull * (uint64_t)count;
+    for (uint64_t t = 0; t < max_tries && found < count; t++) {
+        const int64_t x = (int64_t)(mix64(seed + t) % (uint64_t)g->nv);
+        if (seen.count(x)) continue;
+        int64_t off[2];
+        BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + x, sizeof(off), hipMemcpyDeviceToHost));
+        const int64_t deg = off[1] - off[0];
+        if (deg == 0) continue;
+        if (deg == 1) { // only neighbour may be a self-loop (Graph500: degree >= 1 excluding self-loops)
+            uint32_t nb = 0;
+            BFSX_HIP_TRY(hipMemcpy(&nb, g->d_col + off[0], sizeof(nb), hipMemcpyDeviceToHost));
+            if ((int64_t)nb == x) continue;
+        }
+        seen.insert(x);
+        roots[found++] = x;
+    }
+    if (found < count) return fail(BFSX_E_ARG, "could not sample enough roots with degree >= 1");
+    return BFSX_OK;
+}
+
+int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats) {
+    if (!g) return fail(BFSX_E_ARG, "null graph");
+    const auto t0 = std::chrono::steady_clock::now();
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    bfsx_stats local{};
+    int rc = bfs_run(g, source, &local);
+    if (rc) return rc;
+    if (dist_out || parent_out) {
+        rc = bfs_copy_result(g, dist_out, parent_out);
+        if (rc) return rc;
+    }
+    if (stats) {
+        rc = bfs_mcomp(g, &local.m_comp, &local.reached);
+        if (rc) return rc;
+        local.t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        *stats = local;
+    }
+    return BFSX_OK;
+}
+
+int bfsx_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
+    if (!g) return fail(BFSX_E_ARG, "null graph");
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    return bfs_copy_result(g, dist_out, parent_out);
+}
+
+int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap) {
+    if (!g || (!cum_ms && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    int n = (int)std::min<size_t>(g->level_cum_ms.size(), (size_t)std::max(cap, 0));
+    for (int i = 0; i < n; i++) cum_ms[i] = g->level_cum_ms[i];
+    return n;
+}
+
+int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap) {
+    if (!g || (!dirs && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    int n = (int)std::min<size_t>(g->level_dirs.size(), (size_t)std::max(cap, 0));
+    for (int i = 0; i < n; i++) dirs[i] = g->level_dirs[i];
+    return n;
+}
+
+int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap) {
+    if (!g || (!out && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    int n = (int)std::min<size_t>(g->level_stats.size(), (size_t)std::max(cap, 0));
+    for (int i = 0; i < n; i++) out[i] = g->level_stats[i];
+    return n;
+}
+
+int bfsx_device_synchronize(bfsx_ctx *ctx) {
+    if (!ctx) return fail(BFSX_E_ARG, "null ctx");
+    BFSX_HIP_TRY(hipSetDevice(ctx->device));
+    BFSX_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return BFSX_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,81 @@
+// bfsx_internal.h -- shared declarations of the MI355X BFS engine (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/bfsx.h"
+
+namespace bfsx {
+
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define BFSX_HIP_TRY(call)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return ::bfsx::fail(e_ == hipErrorOutOfMemory ? BFSX_E_OOM : BFSX_E_HIP,         \
+                                std::string(#call) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+// One 64-byte slot of the per-level counter ring (3 slots, see DESIGN.md "Level loop").
+// Level L reads slot L%3 (its own frontier, already on the host), accumulates the frontier it
+// produces into slot (L+1)%3 and zeroes slot (L+2)%3 -- so no per-level memset is needed.
+struct alignas(64) LevelCounters {
+    unsigned long long nf;   // vertices in the produced frontier
+    unsigned long long mf;   // sum of their degrees (Beamer m_f)
+    unsigned long long nhub; // top-down: frontier vertices deferred to the multi-workgroup bin
+    unsigned long long aux;  // scratch (bitmap->queue compaction cursor)
+    unsigned long long scanned; // bottom-up: adjacency entries read (algorithmic-bytes accounting)
+    unsigned long long pad[3];
+};
+static_assert(sizeof(LevelCounters) == 64, "counter slot must be one 64-B line");
+
+struct Options {
+    int direction = BFSX_DIR_AUTO;
+    int alpha = 14;            // top-down -> bottom-up when m_f > m_u / alpha
+    int beta = 24;             // bottom-up -> top-down when n_f < n / beta (and shrinking)
+    uint32_t hub_degree = 4096; // degree above which a frontier vertex gets many workgroups
+};
+
+// ---- kernels_build.hip -------------------------------------------------------------------
+// Builds the CSR (sorted, de-duplicated neighbour sets, self-loops kept once) from device tuple
+// arrays.  Takes ownership of nothing; d_u/d_v stay owned by the caller.
+int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
+                     int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt);
+int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
+                       uint32_t *d_v);
+
+// ---- kernels_bfs.hip ---------------------------------------------------------------------
+struct BfsWorkspace;
+int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
+int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
+int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
+void bfs_workspace_free(BfsWorkspace *ws);
+
+} // namespace bfsx
+
+struct bfsx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bfsx::Options opt;
+    int num_cus = 256;
+};
+
+struct bfsx_graph {
+    bfsx_ctx *ctx = nullptr;
+    int64_t nv = 0, nnz = 0, m = 0;
+    int64_t *d_row_off = nullptr; // [nv+1]
+    uint32_t *d_col = nullptr;    // [nnz]
+    uint32_t *d_tuple_cnt = nullptr; // [nv]: input tuples whose first endpoint is v (m_comp)
+    bfsx::BfsWorkspace *ws = nullptr;
+    // most recent BFS
+    int64_t last_source = -1;
+    std::vector<double> level_cum_ms;
+    std::vector<int32_t> level_dirs;
+    std::vector<bfsx_level_stat> level_stats;
+};

@@ -1,0 +1,326 @@
+// kernels_build.hip -- graph construction on the GPU (gfx950).
+//
+// Replaces GraphFileUtil.convert's symmetrise + HashSet dedup (GraphFileUtil.java:60-66, Vertex.java
+// :74-76): tuples (a,b) become the neighbour sets N(a) += b, N(b) += a, with duplicates collapsed and
+// a self-loop kept once.  The result is CSR: row_off int64[nv+1], col uint32[nnz], rows ascending.
+//
+// Pipeline (all on one HIP stream, all HBM-streaming integer work):
+//   K1a count    degree histogram (atomicAdd per endpoint) + tuple count per first endpoint (m_comp)
+//   K1b scan     rocPRIM exclusive scan -> row offsets
+//   K1c scatter  per-row cursors (64-bit atomics) -> unsorted rows
+//   K1d sort     rocPRIM segmented radix sort of every row (chunked below 2^32 entries)
+//   K1e dedup    keep-flags (row head or != predecessor) -> scan -> compact -> new row offsets
+// The Kronecker generator (Graph500 recipe, counter-based RNG) also lives here.
+#include <cstring>
+
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
+#include <algorithm>
+
+#include "bfsx_internal.h"
+
+namespace bfsx {
+
+namespace {
+
+constexpr int kBS = 256;
+
+inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap = 16384) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+__global__ __launch_bounds__(kBS) void k_count(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
+                                               int64_t m, uint32_t *__restrict__ deg,
+                                               uint32_t *__restrict__ tcnt) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
+        uint32_t a = u[i], b = v[i];
+        atomicAdd(&deg[a], 1u);
+        if (a != b) atomicAdd(&deg[b], 1u);
+        atomicAdd(&tcnt[a], 1u);
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_scatter(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
+                                                 int64_t m, unsigned long long *__restrict__ cursor,
+                                                 uint32_t *__restrict__ col) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
+        uint32_t a = u[i], b = v[i];
+        col[atomicAdd(&cursor[a], 1ull)] = b;
+        if (a != b) col[atomicAdd(&cursor[b], 1ull)] = a;
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_mark_heads(const int64_t *__restrict__ off, int64_t nv,
+                                                    uint8_t *__restrict__ keep) {
+    for (int64_t r = (int64_t)blockIdx.x * kBS + threadIdx.x; r < nv; r += (int64_t)gridDim.x * kBS) {
+        int64_t b = off[r];
+        if (off[r + 1] > b) keep[b] = 1;
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_keep(const uint32_t *__restrict__ col, int64_t nnz,
+                                              uint8_t *__restrict__ keep) {
+    for (int64_t j = (int64_t)blockIdx.x * kBS + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * kBS) {
+        if (j == 0) { keep[0] = 1; continue; }
+        if (!keep[j]) keep[j] = col[j] != col[j - 1];
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_compact(const uint32_t *__restrict__ col, const uint8_t *__restrict__ keep,
+                                                 const int64_t *__restrict__ pos, int64_t nnz,
+                                                 uint32_t *__restrict__ out) {
+    for (int64_t j = (int64_t)blockIdx.x * kBS + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * kBS)
+        if (keep[j]) out[pos[j]] = col[j];
+}
+
+__global__ __launch_bounds__(kBS) void k_new_off(const int64_t *__restrict__ off, const int64_t *__restrict__ pos,
+                                                 int64_t nv, int64_t *__restrict__ noff) {
+    for (int64_t r = (int64_t)blockIdx.x * kBS + threadIdx.x; r <= nv; r += (int64_t)gridDim.x * kBS)
+        noff[r] = pos[off[r]];
+}
+
+struct SubBase {
+    int64_t base;
+    __host__ __device__ int64_t operator()(int64_t x) const { return x - base; }
+};
+
+struct U8ToI64 {
+    __host__ __device__ int64_t operator()(uint8_t x) const { return (int64_t)x; }
+};
+
+// ---- Kronecker generator ---------------------------------------------------------------------
+__device__ __host__ inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+struct KronParams {
+    uint64_t sh;       // mix64(seed)
+    uint64_t mask;     // 2^scale - 1
+    uint64_t a1, c1, a2, c2;
+    int s1, s2, scale;
+    uint32_t t_ab, t_an, t_cn;
+};
+
+__device__ inline uint64_t kron_perm(uint64_t x, const KronParams &p) {
+    x = (x * p.a1 + p.c1) & p.mask;
+    x ^= x >> p.s1;
+    x = (x * p.a2 + p.c2) & p.mask;
+    x ^= x >> p.s2;
+    x = (x * p.a1 + p.c2) & p.mask;
+    return x;
+}
+
+__global__ __launch_bounds__(kBS) void k_kronecker(KronParams p, int64_t m, uint32_t *__restrict__ u,
+                                                   uint32_t *__restrict__ v) {
+    for (int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x; k < m; k += (int64_t)gridDim.x * kBS) {
+        uint64_t i = 0, j = 0;
+        for (int ib = 0; ib < p.scale; ib++) {
+            uint64_t r = mix64((((uint64_t)k) << 6 | (uint64_t)ib) ^ p.sh);
+            uint32_t r1 = (uint32_t)(r >> 32), r2 = (uint32_t)r;
+            uint64_t ii = r1 > p.t_ab;
+            uint64_t jj = r2 > (ii ? p.t_cn : p.t_an);
+            i |= ii << ib;
+            j |= jj << ib;
+        }
+        u[k] = (uint32_t)kron_perm(i, p);
+        v[k] = (uint32_t)kron_perm(j, p);
+    }
+}
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t n) { return hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    }
+    T *release() {
+        T *q = p;
+        p = nullptr;
+        return q;
+    }
+};
+
+} // namespace
+
+int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
+                       uint32_t *d_v) {
+    KronParams p;
+    p.scale = scale;
+    p.sh = mix64(seed);
+    p.mask = (1ULL << scale) - 1;
+    p.a1 = (mix64(seed ^ 0xA5A5A5A5A5A5A5A5ULL) | 1ULL) & p.mask;
+    p.c1 = mix64(seed ^ 0x5A5A5A5A5A5A5A5AULL) & p.mask;
+    p.a2 = (mix64(seed ^ 0x3C3C3C3C3C3C3C3CULL) | 1ULL) & p.mask;
+    p.c2 = mix64(seed ^ 0xC3C3C3C3C3C3C3C3ULL) & p.mask;
+    p.s1 = scale / 2 + 1;
+    p.s2 = scale / 3 + 1;
+    // A,B,C,D = .57,.19,.19,.05: ab = .76, a_norm = 57/76, c_norm = 19/24, as 2^-32 fractions
+    p.t_ab = (uint32_t)((76ULL << 32) / 100ULL);
+    p.t_an = (uint32_t)((57ULL << 32) / 76ULL);
+    p.t_cn = (uint32_t)((19ULL << 32) / 24ULL);
+    int64_t m = (int64_t)edgefactor << scale;
+    hipLaunchKernelGGL(k_kronecker, dim3(grid_for(m, kBS, 32768)), dim3(kBS), 0, stream, p, m, d_u, d_v);
+    BFSX_HIP_TRY(hipGetLastError());
+    return BFSX_OK;
+}
+
+int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
+                     int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out,
+                     uint32_t **d_tuple_cnt_out) {
+    DevBuf<uint32_t> deg, tcnt;
+    DevBuf<int64_t> off;
+    BFSX_HIP_TRY(deg.alloc(nv + 1));
+    BFSX_HIP_TRY(tcnt.alloc(nv));
+    BFSX_HIP_TRY(off.alloc(nv + 1));
+    BFSX_HIP_TRY(hipMemsetAsync(deg.p, 0, (nv + 1) * sizeof(uint32_t), stream));
+    BFSX_HIP_TRY(hipMemsetAsync(tcnt.p, 0, nv * sizeof(uint32_t), stream));
+    if (m > 0) {
+        hipLaunchKernelGGL(k_count, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, deg.p, tcnt.p);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    // K1b: row offsets (int64) = exclusive scan of degrees
+    {
+        size_t tmp_bytes = 0;
+        BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, deg.p, off.p, (int64_t)0, (size_t)(nv + 1),
+                                             rocprim::plus<int64_t>(), stream));
+        DevBuf<char> tmp;
+        BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
+        BFSX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, deg.p, off.p, (int64_t)0, (size_t)(nv + 1),
+                                             rocprim::plus<int64_t>(), stream));
+    }
+    int64_t nnz_raw = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&nnz_raw, off.p + nv, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+    BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    deg.reset();
+
+    // K1c: scatter into per-row slots
+    DevBuf<uint32_t> col;
+    BFSX_HIP_TRY(col.alloc(nnz_raw));
+    {
+        DevBuf<int64_t> cursor;
+        BFSX_HIP_TRY(cursor.alloc(nv));
+        BFSX_HIP_TRY(hipMemcpyAsync(cursor.p, off.p, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
+        if (m > 0) {
+            hipLaunchKernelGGL(k_scatter, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m,
+                               (unsigned long long *)cursor.p, col.p);
+            BFSX_HIP_TRY(hipGetLastError());
+        }
+        BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    }
+
+    // K1d: sort every row (segmented radix sort), in row chunks of < 2^31 entries
+    DevBuf<uint32_t> col_s;
+    BFSX_HIP_TRY(col_s.alloc(nnz_raw));
+    if (nnz_raw > 0) {
+        unsigned end_bit = 1;
+        while (end_bit < 32 && (1ULL << end_bit) < (uint64_t)nv) end_bit++;
+        std::vector<int64_t> h_off;
+        const int64_t kChunk = (int64_t)1 << 31;
+        std::vector<int64_t> row_cuts{0};
+        if (nnz_raw >= kChunk) {
+            h_off.resize(nv + 1);
+            BFSX_HIP_TRY(hipMemcpy(h_off.data(), off.p, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+            int64_t r = 0;
+            while (r < nv) {
+                int64_t limit = h_off[r] + kChunk - 1;
+                int64_t r2 = std::upper_bound(h_off.begin() + r, h_off.end(), limit) - h_off.begin() - 1;
+                if (r2 <= r) return fail(BFSX_E_ARG, "a single adjacency row exceeds 2^31 entries");
+                r2 = std::min<int64_t>(r2, nv);
+                row_cuts.push_back(r2);
+                r = r2;
+            }
+        } else {
+            row_cuts.push_back(nv);
+        }
+        DevBuf<char> tmp;
+        size_t tmp_cap = 0;
+        for (size_t c = 0; c + 1 < row_cuts.size(); c++) {
+            int64_t r0 = row_cuts[c], r1 = row_cuts[c + 1];
+            int64_t e0, e1;
+            if (!h_off.empty()) {
+                e0 = h_off[r0];
+                e1 = h_off[r1];
+            } else {
+                e0 = 0;
+                e1 = nnz_raw;
+            }
+            if (e1 == e0) continue;
+            auto beg = rocprim::make_transform_iterator(off.p + r0, SubBase{e0});
+            auto end = rocprim::make_transform_iterator(off.p + r0 + 1, SubBase{e0});
+            size_t tmp_bytes = 0;
+            BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, col.p + e0, col_s.p + e0,
+                                                            (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end,
+                                                            0, end_bit, stream));
+            if (tmp_bytes > tmp_cap) {
+                tmp.reset();
+                BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
+                tmp_cap = tmp_bytes;
+            }
+            BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(tmp.p, tmp_bytes, col.p + e0, col_s.p + e0,
+                                                            (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end,
+                                                            0, end_bit, stream));
+        }
+        BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    }
+    col.reset(); // unsorted rows are no longer needed
+
+    // K1e: dedup
+    DevBuf<uint8_t> keep;
+    DevBuf<int64_t> pos;
+    BFSX_HIP_TRY(keep.alloc(nnz_raw + 1));
+    BFSX_HIP_TRY(pos.alloc(nnz_raw + 1));
+    BFSX_HIP_TRY(hipMemsetAsync(keep.p, 0, nnz_raw + 1, stream));
+    hipLaunchKernelGGL(k_mark_heads, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, off.p, nv, keep.p);
+    BFSX_HIP_TRY(hipGetLastError());
+    if (nnz_raw > 0) {
+        hipLaunchKernelGGL(k_keep, dim3(grid_for(nnz_raw, kBS)), dim3(kBS), 0, stream, col_s.p, nnz_raw, keep.p);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    {
+        auto in = rocprim::make_transform_iterator(keep.p, U8ToI64{});
+        size_t tmp_bytes = 0;
+        BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, in, pos.p, (int64_t)0, (size_t)(nnz_raw + 1),
+                                             rocprim::plus<int64_t>(), stream));
+        DevBuf<char> tmp;
+        BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
+        BFSX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, in, pos.p, (int64_t)0, (size_t)(nnz_raw + 1),
+                                             rocprim::plus<int64_t>(), stream));
+    }
+    int64_t nnz = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&nnz, pos.p + nnz_raw, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+    BFSX_HIP_TRY(hipStreamSynchronize(stream));
+
+    DevBuf<uint32_t> col_f;
+    DevBuf<int64_t> noff;
+    BFSX_HIP_TRY(col_f.alloc(nnz));
+    BFSX_HIP_TRY(noff.alloc(nv + 1));
+    if (nnz_raw > 0) {
+        hipLaunchKernelGGL(k_compact, dim3(grid_for(nnz_raw, kBS)), dim3(kBS), 0, stream, col_s.p, keep.p, pos.p,
+                           nnz_raw, col_f.p);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_new_off, dim3(grid_for(nv + 1, kBS)), dim3(kBS), 0, stream, off.p, pos.p, nv, noff.p);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipStreamSynchronize(stream));
+
+    *d_row_off_out = noff.release();
+    *d_col_out = col_f.release();
+    *d_tuple_cnt_out = tcnt.release();
+    *nnz_out = nnz;
+    return BFSX_OK;
+}
+
+} // namespace bfsx

@@ -1,0 +1,146 @@
+/*
+ * bfsx.h -- C-ABI of the MI355X-native BFS engine (libbfsx.so).
+ *
+ * The reference (NorthernDemon/BFS-with-MapReduce) has no FFI: its hot path is the per-problem-file
+ * block of BfsSpark.main (src/main/java/it/unitn/bd/bfs/BfsSpark.java:55-118) -- the loader call
+ * GraphFileUtil.convert (GraphFileUtil.java:45-69), then the map/reduceByKey level loop whose
+ * mapper (BfsSpark.java:66-87) and reducer (BfsSpark.java:90-108) are Spark function objects.
+ * Each entry point below names the reference code it replaces.  INTEGRATION.md shows the JNI /
+ * Panama binding a maintainer adds to call these from BfsSpark.main.
+ *
+ * Conventions
+ *   - Every int-returning function returns BFSX_OK (0) or a negative BFSX_E_* code; a message for
+ *     the calling thread is available from bfsx_last_error().  No C++ exception crosses the ABI.
+ *   - Handles are library-owned; free them with the matching *_free / bfsx_finalize.
+ *   - Output arrays are caller-allocated HOST memory of length bfsx_graph_nv().
+ *   - Distances: int32, INT32_MAX (2147483647) = unreachable, exactly the reference's
+ *     Integer.MAX_VALUE initial distance (GraphFileUtil.java:55) that survives for WHITE vertices.
+ *   - Parents: int64, -1 = unreachable, parent[source] = source.
+ *   - A bfsx_ctx is used by one host thread at a time (like the single driver thread of
+ *     BfsSpark.main); bfsx_bfs is synchronous.
+ */
+#ifndef BFSX_H
+#define BFSX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BFSX_ABI_VERSION 1
+
+/* Error codes.  Mapping to the reference's exceptions:
+ *   E_IO    <- IOException from FileInputStream / Files.write  (GraphFileUtil.java:43,46,68)
+ *   E_PARSE <- NumberFormatException / IndexOutOfBoundsException (GraphFileUtil.java:48,61-63)
+ *   E_RANGE <- NullPointerException for a vertex id outside [0,V)  (GraphFileUtil.java:64-65)  */
+#define BFSX_OK 0
+#define BFSX_E_IO (-1)
+#define BFSX_E_PARSE (-2)
+#define BFSX_E_RANGE (-3)
+#define BFSX_E_HIP (-4)
+#define BFSX_E_RCCL (-5)
+#define BFSX_E_OOM (-6)
+#define BFSX_E_ARG (-7)
+#define BFSX_E_NODEV (-8)
+
+/* Traversal direction policy (bfsx_set_option "direction"). */
+#define BFSX_DIR_AUTO 0     /* direction-optimising (Beamer alpha/beta switch) */
+#define BFSX_DIR_TOPDOWN 1  /* push only: the reference mapper's direction (BfsSpark.java:73-79) */
+#define BFSX_DIR_BOTTOMUP 2 /* pull only */
+
+typedef struct bfsx_ctx bfsx_ctx;
+typedef struct bfsx_graph bfsx_graph;
+
+/* Per-BFS statistics.  levels == the number of map/reduce passes the reference runs for the same
+ * graph and source (BfsSpark.java:61, ecc(source)+1), so "Elapsed time [k]" lines line up. */
+typedef struct bfsx_stats {
+    int32_t levels;          /* map/reduce passes = eccentricity(source) + 1 */
+    int32_t topdown_levels;  /* levels run as push (queue -> queue) */
+    int32_t bottomup_levels; /* levels run as pull (bitmap -> bitmap) */
+    int32_t reserved0;
+    int64_t reached;         /* vertices with finite distance (BLACK at the end) */
+    int64_t m_comp;          /* input edge tuples inside the source's component (TEPS numerator) */
+    int64_t edges_examined;  /* sum of frontier degrees over top-down levels + probes (approximate) */
+    double t_bfs_ms;         /* device time: source init -> last level complete (hipEvents) */
+    double t_total_ms;       /* host wall time of the whole call incl. D2H of outputs */
+} bfsx_stats;
+
+/* Per-level record of the most recent bfsx_bfs (diagnostics and roofline accounting). */
+typedef struct bfsx_level_stat {
+    int32_t direction;     /* BFSX_DIR_TOPDOWN or BFSX_DIR_BOTTOMUP */
+    int32_t level;         /* 0-based: expands the vertices at distance `level` */
+    int64_t frontier_in;   /* vertices in the frontier being expanded (GRAY before the pass) */
+    int64_t frontier_out;  /* vertices discovered (GRAY after the pass) */
+    int64_t mf_in;         /* sum of frontier degrees (top-down edges scanned) */
+    int64_t unvisited_in;  /* WHITE vertices before the pass (bottom-up candidates) */
+    int64_t scanned;       /* adjacency entries read (top-down: mf_in; bottom-up: counted) */
+    double kernel_ms;      /* device time of this level's kernels (hipEvents around them) */
+    double cum_ms;         /* device time since source init, like the reference's Stopwatch */
+} bfsx_level_stat;
+
+/* ---- library / context ---------------------------------------------------------------------- */
+int bfsx_abi_version(void);
+const char *bfsx_last_error(void);
+/* Replaces: new JavaSparkContext(...) + spark.addJar (BfsSpark.java:50-51). device = HIP ordinal. */
+int bfsx_init(int device, bfsx_ctx **out);
+void bfsx_finalize(bfsx_ctx *ctx);
+/* Options (all optional; defaults preserve reference behaviour):
+ *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 14) ; "beta" = int (default 24)
+ *   "hub_degree" = int (top-down multi-workgroup bin threshold, default 4096) */
+int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
+
+/* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */
+/* GraphFileUtil.convert's parse (GraphFileUtil.java:46-66): line 1 = V (Integer.parseInt, no trim),
+ * line 2 ignored, every further line split on single spaces, tokens 0 and 1 parsed, read to EOF.
+ * Vertex 0 always exists (GraphFileUtil.java:53), so nv = max(V,1).  Arrays are malloc'd by the
+ * library; release with bfsx_free_host. */
+int bfsx_parse_algs4(const char *path, int64_t *nv, int64_t *m, uint32_t **u, uint32_t **v);
+void bfsx_free_host(void *p);
+
+/* ---- graph construction (device-resident CSR) ------------------------------------------------ */
+/* Replaces GraphFileUtil.convert (GraphFileUtil.java:45-69): parse + symmetrise + dedup into
+ * neighbour sets, built as CSR on the GPU.  Self-loops are kept once (HashSet semantics). */
+int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out);
+/* Same construction from an in-memory tuple list (host arrays of length m, ids < nv). */
+int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
+                          bfsx_graph **out);
+/* Graph500 Kronecker graph (A,B,C,D=.57,.19,.19,.05), generated and built on the GPU.
+ * n = 2^scale, m = edgefactor * n tuples; deterministic in (scale, edgefactor, seed). */
+int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, bfsx_graph **out);
+/* Copy the generator's tuples to host arrays of length edgefactor<<scale (parity testing). */
+int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, uint32_t *u,
+                         uint32_t *v);
+void bfsx_graph_free(bfsx_graph *g);
+
+int64_t bfsx_graph_nv(const bfsx_graph *g);  /* vertices */
+int64_t bfsx_graph_nnz(const bfsx_graph *g); /* directed adjacency entries after dedup */
+int64_t bfsx_graph_m(const bfsx_graph *g);   /* input tuples */
+/* D2H copy of the CSR: row_off[nv+1], col[nnz] (either may be NULL). Rows sorted ascending. */
+int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col);
+/* Graph500 root sampling: count distinct vertices with a non-self-loop neighbour, seeded. */
+int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots);
+
+/* ---- the hot path ---------------------------------------------------------------------------- */
+/* Replaces the level loop BfsSpark.java:57-118: mapper (frontier expansion, :66-87), reducer
+ * (min distance / darkest colour, :90-108), collect + termination test (:110-117).
+ * dist_out / parent_out may be NULL (results stay on the device, e.g. inside a timed region). */
+int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats);
+/* Copy the most recent bfsx_bfs result of this graph to host (same layout as bfsx_bfs outputs). */
+int bfsx_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
+/* Device time of each level of the most recent bfsx_bfs, cumulative like the reference's
+ * Stopwatch (BfsSpark.java:59,63,111-112).  Returns the number of levels written (<= cap). */
+int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap);
+/* Per-level direction of the most recent bfsx_bfs (BFSX_DIR_TOPDOWN / BFSX_DIR_BOTTOMUP). */
+int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap);
+
+/* Per-level records of the most recent bfsx_bfs.  Returns the number written (<= cap). */
+int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap);
+
+/* ---- device synchronisation helper for benchmarking harnesses ------------------------------- */
+int bfsx_device_synchronize(bfsx_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

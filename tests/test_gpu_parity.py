@@ -1,0 +1,195 @@
+"""GPU parity tests: libbfsx.so on cuda:0 against the CPU oracle and the committed golden vectors.
+
+Distances must be bit-exact (integer work); parent trees are validated (Graph500 rules +
+BreadthFirstPaths.check), not compared, because the reference's own tie-break is shuffle-order
+dependent (BfsSpark.java:97)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+INF = 2147483647
+
+
+def read_dist(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return np.array([int(line.split()[1]) for line in f], dtype=np.int32)
+
+
+def check_against_oracle(g, nv, off, col, src, u=None, v=None, mr=True):
+    dist, parent, st = g.bfs(src)
+    if mr:
+        r = O.mapreduce_bfs(nv, off, col, src)
+        ref = r["dist"]
+        assert st["levels"] == r["iters"]
+    else:
+        ref, _ = O.csr_bfs(nv, off, col, src)
+        assert st["levels"] == int(ref[ref != INF].max()) + 1
+    assert np.array_equal(dist, ref)
+    assert O.validate(nv, off, col, src, dist, parent) == 0
+    assert st["reached"] == int((ref != INF).sum())
+    if u is not None:
+        assert st["m_comp"] == O.mcomp(u, v, ref)
+    return dist, parent, st
+
+
+@pytest.mark.parametrize("name", ["tinyCG", "mediumG", "tinyG"])
+@pytest.mark.parametrize("direction", ["auto", "topdown", "bottomup"])
+def test_reference_test_sets_bit_exact(ctx, name, direction):
+    ctx.set_option("direction", direction)
+    try:
+        path = os.path.join(GOLDEN, name + ".txt")
+        nv, u, v = O.load_graphfileutil(path)
+        off, col = O.build_sets(nv, u, v)
+        with ctx.load_algs4(path) as g:
+            assert g.nv == nv and g.m == len(u) and g.nnz == off[-1]
+            goff, gcol = g.csr()
+            assert np.array_equal(goff, off) and np.array_equal(gcol, col)
+            dist, parent, st = check_against_oracle(g, nv, off, col, 0, u, v)
+            assert np.array_equal(dist, read_dist(name + ".dist"))
+            assert O.dist_sha256(dist) == O.dist_sha256(read_dist(name + ".dist"))
+            assert st["levels"] == {"tinyCG": 3, "mediumG": 14, "tinyG": 3}[name]
+            t = g.level_times()
+            assert len(t) == st["levels"] and np.all(np.diff(t) >= 0)
+    finally:
+        ctx.set_option("direction", "auto")
+
+
+def test_tinycg_every_source(ctx):
+    path = os.path.join(GOLDEN, "tinyCG.txt")
+    nv, u, v = O.load_graphfileutil(path)
+    off, col = O.build_sets(nv, u, v)
+    with ctx.load_algs4(path) as g:
+        for s in range(nv):
+            check_against_oracle(g, nv, off, col, s, u, v)
+
+
+def random_cases():
+    rng = np.random.default_rng(2026)
+    cases = []
+    # (name, nv, u, v)
+    for i in range(12):
+        nv = int(rng.integers(1, 3000))
+        m = int(rng.integers(0, 6 * nv + 1))
+        cases.append((f"rand{i}", nv, rng.integers(0, nv, m), rng.integers(0, nv, m)))
+    n = 5000
+    cases.append(("path", n, np.arange(n - 1), np.arange(1, n)))             # deep: 5000 levels
+    cases.append(("star", 20000, np.zeros(19999, int), np.arange(1, 20000)))  # hub bin
+    hubs = np.repeat(np.arange(8), 9000)
+    cases.append(("multi_hub", 12000, hubs, rng.integers(0, 12000, hubs.size)))
+    cases.append(("isolated", 1000, np.array([3, 5]), np.array([5, 7])))
+    cases.append(("self_loops", 100, np.arange(100), np.arange(100)))
+    cases.append(("dups", 64, np.tile(np.arange(63), 5), np.tile(np.arange(1, 64), 5)))
+    cases.append(("single", 1, np.zeros(0, int), np.zeros(0, int)))
+    cases.append(("two_comp", 130, np.r_[np.arange(64), np.arange(65, 129)],
+                  np.r_[np.arange(1, 65), np.arange(66, 130)]))
+    return cases
+
+
+@pytest.mark.parametrize("case", random_cases(), ids=lambda c: c[0])
+@pytest.mark.parametrize("direction", ["auto", "topdown", "bottomup"])
+def test_edge_cases_bit_exact(ctx, case, direction):
+    name, nv, u, v = case
+    u = np.asarray(u, np.uint32)
+    v = np.asarray(v, np.uint32)
+    off, col = O.build_sets(nv, u, v)
+    ctx.set_option("direction", direction)
+    try:
+        with ctx.from_edges(nv, u, v) as g:
+            goff, gcol = g.csr()
+            assert np.array_equal(goff, off) and np.array_equal(gcol, col)
+            srcs = {0, nv - 1, nv // 2}
+            for s in sorted(srcs):
+                check_against_oracle(g, nv, off, col, s, u, v, mr=(nv <= 3000))
+    finally:
+        ctx.set_option("direction", "auto")
+
+
+def test_hub_threshold_sweep(ctx):
+    rng = np.random.default_rng(5)
+    nv = 4096
+    u = np.r_[np.zeros(3000, int), rng.integers(0, nv, 20000)].astype(np.uint32)
+    v = np.r_[rng.integers(0, nv, 3000), rng.integers(0, nv, 20000)].astype(np.uint32)
+    off, col = O.build_sets(nv, u, v)
+    ref, _ = O.csr_bfs(nv, off, col, 0)
+    try:
+        for hub in (1, 16, 64, 4096, 1 << 20):
+            ctx.set_option("hub_degree", hub)
+            ctx.set_option("direction", "topdown")
+            with ctx.from_edges(nv, u, v) as g:
+                d, p, _ = g.bfs(0)
+                assert np.array_equal(d, ref)
+                assert O.validate(nv, off, col, 0, d, p) == 0
+    finally:
+        ctx.set_option("hub_degree", 4096)
+        ctx.set_option("direction", "auto")
+
+
+@pytest.mark.parametrize("scale", [8, 12, 16])
+def test_kronecker_generator_bit_exact(ctx, scale):
+    u, v = ctx.kronecker_edges(scale, 16, 0x5EED2026)
+    ou, ov = O.kronecker(scale, 16, 0x5EED2026)
+    assert np.array_equal(u, ou) and np.array_equal(v, ov)
+
+
+@pytest.mark.parametrize("scale", [10, 16])
+def test_kronecker_bfs_parity(ctx, scale):
+    seed = 0xABCD + scale
+    ou, ov = O.kronecker(scale, 16, seed)
+    nv = 1 << scale
+    off, col = O.build_sets(nv, ou, ov)
+    with ctx.kronecker(scale, 16, seed) as g:
+        goff, gcol = g.csr()
+        assert np.array_equal(goff, off) and np.array_equal(gcol, col)
+        roots = g.sample_roots(8, seed=3)
+        assert len(set(roots.tolist())) == 8
+        for r in roots:
+            assert off[r + 1] > off[r]
+            check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=(scale <= 12))
+        dirs = g.level_dirs()
+        assert len(dirs) > 0
+
+
+def test_kronecker_scale20_validated(ctx):
+    """Full-size-style property check: Graph500 validation + oracle distances at scale 20."""
+    scale = 20
+    with ctx.kronecker(scale, 16, 0x5EED2026) as g:
+        nv = g.nv
+        off, col = g.csr()
+        for r in g.sample_roots(4, seed=11):
+            d, p, st = g.bfs(int(r))
+            ref, _ = O.csr_bfs(nv, off, col, int(r))
+            assert np.array_equal(d, ref)
+            assert O.validate(nv, off, col, int(r), d, p) == 0
+            assert st["bottomup_levels"] > 0  # direction optimisation engaged
+            assert st["t_bfs_ms"] > 0
+
+
+def test_errors(ctx, bfsx):
+    with pytest.raises(bfsx.BfsxError) as ei:
+        ctx.load_algs4("/nonexistent.txt")
+    assert ei.value.code == bfsx.BFSX_E_IO
+    with ctx.from_edges(10, np.array([1], np.uint32), np.array([2], np.uint32)) as g:
+        with pytest.raises(bfsx.BfsxError) as ei:
+            g.bfs(10)
+        assert ei.value.code == bfsx.BFSX_E_RANGE
+    with pytest.raises(bfsx.BfsxError) as ei:
+        ctx.from_edges(10, np.array([1], np.uint32), np.array([10], np.uint32))
+    assert ei.value.code == bfsx.BFSX_E_RANGE
+    with pytest.raises(bfsx.BfsxError):
+        ctx.set_option("direction", "sideways")
+
+
+def test_repeated_bfs_reuses_state(ctx):
+    path = os.path.join(GOLDEN, "mediumG.txt")
+    with ctx.load_algs4(path) as g:
+        d0, _, _ = g.bfs(0)
+        for s in (5, 77, 249, 0):
+            d, p, _ = g.bfs(s)
+        assert np.array_equal(d, d0)
+        d2, p2 = g.result()
+        assert np.array_equal(d2, d0)
