@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--direction", default="auto")
     ap.add_argument("--levels-json", default="")
+    ap.add_argument("--option", action="append", default=[], help="libbfsx option key=value")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -73,6 +74,9 @@ def main():
             dist_mod.barrier()
 
     ctx = bfsx.Context(local_rank, direction=args.direction)
+    for kv in args.option:
+        k, val = kv.split("=", 1)
+        ctx.set_option(k, val)
     t0 = time.perf_counter()
     g = ctx.kronecker(args.scale, args.edgefactor, args.seed)
     build_s = time.perf_counter() - t0

@@ -222,6 +222,18 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "direction must be auto|topdown|bottomup");
         return BFSX_OK;
     }
+    if (k == "row_order") {
+        if (v == "degree") ctx->opt.degree_order = true;
+        else if (v == "id") ctx->opt.degree_order = false;
+        else return fail(BFSX_E_ARG, "row_order must be degree|id");
+        return BFSX_OK;
+    }
+    if (k == "td_probe") {
+        if (v == "plain") ctx->opt.agent_probe = false;
+        else if (v == "agent") ctx->opt.agent_probe = true;
+        else return fail(BFSX_E_ARG, "td_probe must be plain|agent");
+        return BFSX_OK;
+    }
     if (k == "alpha") return as_int(ctx->opt.alpha);
     if (k == "beta") return as_int(ctx->opt.beta);
     if (k == "hub_degree") {
@@ -240,7 +252,8 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
     g->ctx = ctx;
     g->nv = nv;
     g->m = m;
-    int rc = build_csr_device(ctx->stream, nv, d_u, d_v, m, &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt);
+    int rc = build_csr_device(ctx->stream, nv, d_u, d_v, m, ctx->opt.degree_order, &g->d_row_off, &g->d_col,
+                              &g->nnz, &g->d_tuple_cnt);
     if (rc) {
         delete g;
         return rc;

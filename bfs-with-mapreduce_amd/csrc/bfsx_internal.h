@@ -31,7 +31,8 @@ struct alignas(64) LevelCounters {
     unsigned long long nhub; // top-down: frontier vertices deferred to the multi-workgroup bin
     unsigned long long aux;  // scratch (bitmap->queue compaction cursor)
     unsigned long long scanned; // bottom-up: adjacency entries read (algorithmic-bytes accounting)
-    unsigned long long pad[3];
+    unsigned long long claims;  // top-down: atomicOr claims attempted (diagnostics)
+    unsigned long long pad[2];
 };
 static_assert(sizeof(LevelCounters) == 64, "counter slot must be one 64-B line");
 
@@ -39,14 +40,17 @@ struct Options {
     int direction = BFSX_DIR_AUTO;
     int alpha = 14;            // top-down -> bottom-up when m_f > m_u / alpha
     int beta = 24;             // bottom-up -> top-down when n_f < n / beta (and shrinking)
-    uint32_t hub_degree = 4096; // degree above which a frontier vertex gets many workgroups
+    uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
+    bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
+    bool agent_probe = false;   // top-down visited probe: agent-scope (L1-bypassing) load vs plain
 };
 
 // ---- kernels_build.hip -------------------------------------------------------------------
 // Builds the CSR (sorted, de-duplicated neighbour sets, self-loops kept once) from device tuple
 // arrays.  Takes ownership of nothing; d_u/d_v stay owned by the caller.
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
-                     int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt);
+                     bool degree_order, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
+                     uint32_t **d_tuple_cnt);
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v);
 

@@ -22,6 +22,9 @@ struct BfsWorkspace {
     int64_t nv = 0, nwords = 0;
     int32_t *dist = nullptr, *parent = nullptr;
     unsigned long long *vis = nullptr, *front = nullptr, *next = nullptr;
+    unsigned long long *dead = nullptr; // isolated vertices + padding (initial visited bitmap)
+    uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex
+    int64_t n_dead = 0;                 // isolated vertices (excluding padding)
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
     LevelCounters *ring = nullptr;   // device, 4 slots (3 ring + 1 scratch)
     LevelCounters *h_ring = nullptr; // pinned host mirror of one slot
@@ -53,33 +56,6 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
     return x;
 }
 
-// Claim vertex v in the visited bitmap.  A plain load first filters already-visited vertices (bits
-// only ever get set, so a stale line can only under-report); the atomicOr decides the race.
-__device__ inline bool try_claim(uint32_t v, unsigned long long *vis) {
-    const unsigned long long bit = 1ull << (v & 63u);
-    unsigned long long *w = vis + (v >> 6);
-    if (*w & bit) return false;
-    return !(atomicOr(w, bit) & bit);
-}
-
-// Wave-collective append of the winners to the next queue: one ballot, one atomic per wave.
-// Must be called by all 64 lanes (wave-uniform control flow).
-__device__ inline void wave_append(bool win, uint32_t v, unsigned long long vdeg, uint32_t *__restrict__ q,
-                                   LevelCounters *c) {
-    const unsigned long long mask = __ballot(win);
-    if (mask == 0) return;
-    const unsigned lane = lane_id();
-    const int leader = __ffsll((long long)mask) - 1;
-    const unsigned long long dsum = wave_sum(win ? vdeg : 0ull);
-    uint32_t base = 0;
-    if ((int)lane == leader) {
-        base = (uint32_t)atomicAdd(&c->nf, (unsigned long long)__popcll(mask));
-        atomicAdd(&c->mf, dsum);
-    }
-    base = __shfl(base, leader);
-    if (win) q[base + __popcll(mask & ((1ull << lane) - 1ull))] = v;
-}
-
 __device__ inline void zero_slot(LevelCounters *ring, int level) {
     if (blockIdx.x == 0 && threadIdx.x < 8)
         reinterpret_cast<unsigned long long *>(ring + (level + 2) % 3)[threadIdx.x] = 0ull;
@@ -91,19 +67,146 @@ __global__ void k_init_source(uint32_t s, const int64_t *__restrict__ row_off, i
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         dist[s] = 0;
         parent[s] = (int32_t)s;
-        vis[s >> 6] = 1ull << (s & 63u);
+        vis[s >> 6] |= 1ull << (s & 63u);
         q[0] = s;
         ring[0].nf = 1;
         ring[0].mf = (unsigned long long)(row_off[s + 1] - row_off[s]);
-        ring[3].pad[0] = ring[0].mf;
     }
 }
 
-// ---- K3: top-down push, workgroup-balanced -----------------------------------------------------
-// Each workgroup takes 256 frontier vertices, scans their degrees in LDS and sweeps the union of
-// their adjacency rows edge-parallel (thread / wave / workgroup granularity in one pass: a thread
-// finds its row by binary search in the LDS scan).  Vertices of degree > hub_deg go to the hub list
-// and are swept by every workgroup in k_td_hubs (the multi-workgroup bin).
+// ---- block-level output queue ------------------------------------------------------------------
+// Winners are appended to an LDS buffer (LDS atomics) and flushed to the global next-frontier queue
+// with ONE global atomic per ~kQCap winners: a single device counter hit by every wave serialises
+// at the memory side (measured 2.4 G edges/s on scale 26 with per-wave appends).
+constexpr int kQCap = 4096;
+
+struct BlockQueue {
+    uint32_t buf[kQCap];
+    uint32_t n;
+    uint32_t gbase;
+    unsigned long long mf[kWaves];
+};
+
+// All 64 lanes of every wave call this (wave-uniform control flow).
+__device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
+    const unsigned long long mask = __ballot(win);
+    if (mask == 0) return;
+    const unsigned lane = lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(&q.n, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (win) q.buf[base + __popcll(mask & ((1ull << lane) - 1ull))] = v;
+}
+
+// Block-uniform: every thread calls after a __syncthreads().
+__device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, LevelCounters *cn) {
+    const uint32_t n = q.n;
+    if (n == 0) return;
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(&cn->nf, (unsigned long long)n);
+    __syncthreads();
+    const uint32_t gb = q.gbase;
+    for (uint32_t i = threadIdx.x; i < n; i += kBS) qout[gb + i] = q.buf[i];
+    __syncthreads();
+    if (threadIdx.x == 0) q.n = 0;
+    __syncthreads();
+}
+
+__device__ inline void bq_init(BlockQueue &q) {
+    if (threadIdx.x == 0) q.n = 0;
+}
+
+// Block-uniform epilogue: flush the queue and add the block's degree sum to m_f.
+__device__ inline void bq_finish(BlockQueue &q, uint32_t *__restrict__ qout, LevelCounters *cn,
+                                 unsigned long long acc_mf) {
+    acc_mf = wave_sum(acc_mf);
+    if (lane_id() == 0) q.mf[threadIdx.x >> 6] = acc_mf;
+    __syncthreads();
+    bq_flush(q, qout, cn);
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int i = 0; i < kWaves; i++) t += q.mf[i];
+        if (t) atomicAdd(&cn->mf, t);
+    }
+}
+
+// ---- K3: top-down push, degree-binned -----------------------------------------------------------
+// Two bins, chosen per frontier vertex by degree:
+//   k_td       vertex groups: a workgroup takes 256 frontier vertices of degree <= hub_deg, scans
+//              their degrees in LDS and sweeps the union of their rows edge-parallel (a thread finds
+//              its row by binary search in the LDS scan), kItems edges per thread per step so that
+//              several independent loads are in flight.
+//   k_td_hubs  multi-workgroup bin: vertices of degree > hub_deg are appended to a hub list; every
+//              workgroup loads a batch of hubs into LDS, scans their degrees and sweeps an equal
+//              share of the batch's edges, so a single huge row or thousands of medium rows are
+//              spread evenly over the whole grid.
+constexpr int kItems = 4;
+constexpr int kHubBatch = 1024;
+
+template <bool kAgentProbe>
+__device__ inline bool claim(uint32_t v, unsigned long long *vis, unsigned long long &attempts) {
+    const unsigned long long bit = 1ull << (v & 63u);
+    unsigned long long *w = vis + (v >> 6);
+    unsigned long long cur;
+    if (kAgentProbe) cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else cur = *w;
+    if (cur & bit) return false; // bits are only ever set: a stale line can only under-report
+    attempts++;
+    return !(atomicOr(w, bit) & bit);
+}
+
+// Sweep `cnt` edges x0..x0+cnt of a segment table (scan/beg/u in LDS, n entries) in steps of
+// kBS*kItems.  Block-uniform.
+template <bool kAgentProbe, class ScanT>
+__device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
+                                      uint64_t x_begin, uint64_t x_end, const int64_t *__restrict__ row_off,
+                                      const uint32_t *__restrict__ col, unsigned long long *vis,
+                                      int32_t *__restrict__ dist, int32_t *__restrict__ parent, int32_t nd,
+                                      BlockQueue &q, uint32_t *__restrict__ qout, LevelCounters *cn,
+                                      unsigned long long &acc_mf, unsigned long long &attempts) {
+    for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
+        uint32_t v[kItems], pu[kItems];
+        bool valid[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            const uint64_t x = x0 + (uint64_t)k * kBS + threadIdx.x;
+            valid[k] = x < x_end;
+            v[k] = 0;
+            pu[k] = 0;
+            if (valid[k]) {
+                int lo = 0, hi = n - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((uint64_t)s_scan[mid] <= x) lo = mid;
+                    else hi = mid - 1;
+                }
+                v[k] = col[s_beg[lo] + (int64_t)(x - (uint64_t)s_scan[lo])];
+                pu[k] = s_u[lo];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            bool win = false;
+            if (valid[k] && claim<kAgentProbe>(v[k], vis, attempts)) {
+                win = true;
+                dist[v[k]] = nd;
+                parent[v[k]] = (int32_t)pu[k];
+                acc_mf += (unsigned long long)(row_off[v[k] + 1] - row_off[v[k]]);
+            }
+            bq_push(q, win, v[k]);
+        }
+        __syncthreads();
+        if (q.n > (uint32_t)(kQCap - kBS * kItems)) bq_flush(q, qout, cn);
+    }
+}
+
+__device__ inline void add_attempts(LevelCounters *cn, unsigned long long attempts) {
+    attempts = wave_sum(attempts);
+    if (lane_id() == 0 && attempts) atomicAdd(&cn->claims, attempts);
+}
+
+template <bool kAgentProbe>
 __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, unsigned long long *vis,
@@ -116,8 +219,11 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
     __shared__ int64_t s_beg[kBS];
     __shared__ uint32_t s_u[kBS];
     __shared__ uint32_t s_wsum[kWaves];
+    __shared__ BlockQueue q;
+    bq_init(q);
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    unsigned long long acc_mf = 0, attempts = 0;
     for (uint32_t base = blockIdx.x * kBS; base < qlen; base += gridDim.x * kBS) {
         const uint32_t i = base + tid;
         uint32_t deg = 0, u = 0;
@@ -147,69 +253,106 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
         s_u[tid] = u;
         if (tid == 0) s_scan[kBS] = total;
         __syncthreads();
-        for (uint32_t e0 = 0; e0 < total; e0 += kBS) {
-            const uint32_t e = e0 + tid;
-            bool win = false;
-            uint32_t v = 0;
-            unsigned long long vdeg = 0;
-            if (e < total) {
-                int lo = 0, hi = kBS - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_scan[mid] <= e) lo = mid;
-                    else hi = mid - 1;
-                }
-                v = col[s_beg[lo] + (e - s_scan[lo])];
-                if (try_claim(v, vis)) {
-                    win = true;
-                    dist[v] = nd;
-                    parent[v] = (int32_t)s_u[lo];
-                    vdeg = (unsigned long long)(row_off[v + 1] - row_off[v]);
-                }
-            }
-            wave_append(win, v, vdeg, qout, cn);
-        }
+        sweep_segments<kAgentProbe>(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, dist, parent, nd, q, qout,
+                                    cn, acc_mf, attempts);
         __syncthreads();
     }
+    add_attempts(cn, attempts);
+    bq_finish(q, qout, cn, acc_mf);
 }
 
-// Multi-workgroup bin: every workgroup sweeps a strided slice of each hub's row.
+template <bool kAgentProbe>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row_off,
                                                  const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  unsigned long long *vis, int32_t *__restrict__ dist,
                                                  int32_t *__restrict__ parent, LevelCounters *ring, int level) {
     LevelCounters *cn = ring + (level + 1) % 3;
+    __shared__ unsigned long long s_scan[kHubBatch + 1];
+    __shared__ int64_t s_beg[kHubBatch];
+    __shared__ uint32_t s_u[kHubBatch];
+    __shared__ unsigned long long s_tsum[kBS];
+    __shared__ BlockQueue q;
+    bq_init(q);
     const uint32_t nh = (uint32_t)cn->nhub;
     const int32_t nd = level + 1;
-    for (uint32_t h = 0; h < nh; h++) {
-        const uint32_t u = hubs[h];
-        const int64_t beg = row_off[u], deg = row_off[u + 1] - beg;
-        for (int64_t e0 = (int64_t)blockIdx.x * kBS; e0 < deg; e0 += (int64_t)gridDim.x * kBS) {
-            const int64_t e = e0 + threadIdx.x;
-            bool win = false;
-            uint32_t v = 0;
-            unsigned long long vdeg = 0;
-            if (e < deg) {
-                v = col[beg + e];
-                if (try_claim(v, vis)) {
-                    win = true;
-                    dist[v] = nd;
-                    parent[v] = (int32_t)u;
-                    vdeg = (unsigned long long)(row_off[v + 1] - row_off[v]);
-                }
+    const unsigned tid = threadIdx.x;
+    constexpr int kPer = kHubBatch / kBS;
+    unsigned long long acc_mf = 0, attempts = 0;
+    __syncthreads();
+    for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
+        const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
+        // thread tid owns batch entries [tid*kPer, tid*kPer+kPer): load degrees, local sum
+        unsigned long long d[kPer], local = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int idx = (int)tid * kPer + k;
+            d[k] = 0;
+            if (idx < hb) {
+                const uint32_t u = hubs[h0 + idx];
+                const int64_t b = row_off[u];
+                d[k] = (unsigned long long)(row_off[u + 1] - b);
+                s_beg[idx] = b;
+                s_u[idx] = u;
             }
-            wave_append(win, v, vdeg, qout, cn);
+            local += d[k];
         }
+        s_tsum[tid] = local;
+        __syncthreads();
+        // block exclusive scan of the per-thread sums (256 entries, Hillis-Steele in LDS)
+        for (int off = 1; off < kBS; off <<= 1) {
+            const unsigned long long add = tid >= (unsigned)off ? s_tsum[tid - off] : 0ull;
+            __syncthreads();
+            s_tsum[tid] += add;
+            __syncthreads();
+        }
+        unsigned long long run = s_tsum[tid] - local;
+        const unsigned long long total = s_tsum[kBS - 1];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int idx = (int)tid * kPer + k;
+            if (idx < kHubBatch) s_scan[idx] = (idx < hb) ? run : total;
+            run += d[k];
+        }
+        if (tid == 0) s_scan[kHubBatch] = total;
+        __syncthreads();
+        // this workgroup's equal share of the batch's edges
+        const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
+        sweep_segments<kAgentProbe>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, dist, parent, nd,
+                                    q, qout, cn, acc_mf, attempts);
+        __syncthreads();
     }
+    add_attempts(cn, attempts);
+    bq_finish(q, qout, cn, acc_mf);
 }
 
 // ---- K5: bottom-up pull --------------------------------------------------------------------------
-// One wave owns one 64-vertex word of the visited bitmap: lane l handles vertex 64w+l, so the
-// visited word is one broadcast load, row offsets are a coalesced 512-B read, and the new frontier
-// word / visited word are written by one lane without atomics.  Each unvisited vertex scans its row
-// until it finds a neighbour in the current frontier bitmap.
+// A wave owns 64 consecutive words of the visited bitmap (4096 vertices): one coalesced 512-B load
+// brings them into registers (lane k holds word w0+k).  The unvisited vertices of the group are then
+// compacted lane-densely -- a wave prefix of per-word popcounts, a shuffle binary search for the
+// owning word and a popcount bit-select -- so every lane works on a live candidate, whether the
+// level leaves half the vertices unvisited or one in a hundred.  The first probe of a candidate reads
+// top1[v] (its highest-degree neighbour, stored densely: a coalesced wave load for consecutive
+// candidates instead of scattered adjacency lines); only on a miss does the lane walk the rest of
+// its row, four entries per step (independent loads in flight).  Found bits are OR-ed into a
+// per-wave LDS copy of the 64 next-frontier words and written back coalesced with the visited words.
+__device__ inline int select_bit(unsigned long long x, int r) { // position of the r-th set bit (r < popc)
+    int pos = 0;
+#pragma unroll
+    for (int half = 32; half >= 1; half >>= 1) {
+        const unsigned long long lowmask = (half == 64) ? ~0ull : ((1ull << half) - 1ull);
+        const int c = __popcll(x & lowmask);
+        if (r >= c) {
+            r -= c;
+            x >>= half;
+            pos += half;
+        }
+    }
+    return pos;
+}
+
 __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                            const uint32_t *__restrict__ top1,
                                             const unsigned long long *__restrict__ front,
                                             unsigned long long *__restrict__ next,
                                             unsigned long long *__restrict__ vis, int32_t *__restrict__ dist,
@@ -218,43 +361,91 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
     LevelCounters *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ unsigned long long s_nf[kWaves], s_mf[kWaves], s_sc[kWaves];
+    __shared__ unsigned long long s_nx[kWaves][64];
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
     unsigned long long acc_nf = 0, acc_mf = 0, acc_sc = 0;
-    for (int64_t w = (int64_t)blockIdx.x * kWaves + wave; w < nwords; w += (int64_t)gridDim.x * kWaves) {
-        const unsigned long long vw = vis[w];
-        const int64_t v = w * 64 + lane;
-        bool found = false;
-        uint32_t par = 0;
-        unsigned long long deg = 0, scanned = 0;
-        if (v < nv && !((vw >> lane) & 1ull)) {
-            const int64_t b = row_off[v], e = row_off[v + 1];
-            deg = (unsigned long long)(e - b);
-            int64_t j = b;
-            for (; j < e; j++) {
-                const uint32_t x = col[j];
+    const int64_t wstride = (int64_t)gridDim.x * kWaves * 64;
+    for (int64_t w0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; w0 < nwords; w0 += wstride) {
+        const int64_t wl = w0 + lane;
+        const unsigned long long vwl = wl < nwords ? vis[wl] : ~0ull;
+        const unsigned long long unv = ~vwl;
+        const uint32_t c = (uint32_t)__popcll(unv);
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t total = __shfl(incl, 63);
+        if (total == 0) { // wave-uniform: every vertex of the group visited or isolated
+            if (wl < nwords) next[wl] = 0ull;
+            continue;
+        }
+        const uint32_t excl = incl - c;
+        s_nx[wave][lane] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+            const uint32_t idx = t0 + lane;
+            bool found = false;
+            uint32_t par = 0;
+            int64_t v = 0;
+            unsigned long long deg = 0, scanned = 0;
+            // owning word (largest k with excl[k] <= idx) and bit, computed by every lane (shuffles
+            // need all lanes active); lanes past the end work on a clamped index and are masked below
+            const uint32_t ic = idx < total ? idx : total - 1;
+            int k = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const uint32_t e = __shfl(excl, (k + step) & 63);
+                if (k + step < 64 && e <= ic) k += step;
+            }
+            const unsigned long long uk = __shfl(unv, k);
+            const int bit = select_bit(uk, (int)(ic - __shfl(excl, k)));
+            if (idx < total) {
+                v = (w0 + k) * 64 + bit; // < nv: padding bits are set in the dead mask
+                const int64_t b = row_off[v], e = row_off[v + 1];
+                deg = (unsigned long long)(e - b);
+                const uint32_t x = top1[v];
+                int64_t j = b + 1;
                 if ((front[x >> 6] >> (x & 63u)) & 1ull) {
                     found = true;
                     par = x;
-                    j++;
-                    break;
                 }
+                while (!found && j < e) {
+                    const int64_t left = e - j;
+                    const uint32_t x0 = col[j];
+                    const uint32_t x1 = left > 1 ? col[j + 1] : x0;
+                    const uint32_t x2 = left > 2 ? col[j + 2] : x0;
+                    const uint32_t x3 = left > 3 ? col[j + 3] : x0;
+                    const bool h0 = (front[x0 >> 6] >> (x0 & 63u)) & 1ull;
+                    const bool h1 = (front[x1 >> 6] >> (x1 & 63u)) & 1ull;
+                    const bool h2 = (front[x2 >> 6] >> (x2 & 63u)) & 1ull;
+                    const bool h3 = (front[x3 >> 6] >> (x3 & 63u)) & 1ull;
+                    if (h0 | h1 | h2 | h3) {
+                        found = true;
+                        const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
+                        par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
+                        j += h + 1;
+                    } else {
+                        j += left < 4 ? left : 4;
+                    }
+                }
+                scanned = (unsigned long long)(j - b);
             }
-            scanned = (unsigned long long)(j - b);
+            if (found) {
+                dist[v] = nd;
+                parent[v] = (int32_t)par;
+                atomicOr(&s_nx[wave][k], 1ull << bit);
+                acc_mf += deg;
+                acc_nf += 1;
+            }
+            acc_sc += scanned;
         }
-        const unsigned long long fm = __ballot(found);
-        if (found) {
-            dist[v] = nd;
-            parent[v] = (int32_t)par;
+        __builtin_amdgcn_wave_barrier();
+        const unsigned long long nxl = s_nx[wave][lane];
+        if (wl < nwords) {
+            next[wl] = nxl;
+            if (nxl) vis[wl] = vwl | nxl;
         }
-        if (lane == 0) {
-            next[w] = fm;
-            if (fm) vis[w] = vw | fm;
-        }
-        acc_nf += (unsigned long long)__popcll(fm);
-        acc_mf += wave_sum(found ? deg : 0ull);
-        acc_sc += scanned;
     }
+    acc_nf = wave_sum(acc_nf);
+    acc_mf = wave_sum(acc_mf);
     acc_sc = wave_sum(acc_sc);
     if (lane == 0) {
         s_nf[wave] = acc_nf;
@@ -310,6 +501,42 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const unsigned long lon
     }
 }
 
+// Dead mask: vertices that no BFS can reach from elsewhere (degree 0, or a self-loop only) plus the
+// padding bits of the last word.  The visited bitmap starts as this mask, so bottom-up waves skip
+// words that hold only visited/isolated vertices with one uniform branch.
+__global__ __launch_bounds__(kBS) void k_dead_mask(const int64_t *__restrict__ row_off,
+                                                   const uint32_t *__restrict__ col, int64_t nv, int64_t nwords,
+                                                   unsigned long long *__restrict__ dead) {
+    const unsigned lane = lane_id();
+    for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords; w += ((int64_t)gridDim.x * kBS) >> 6) {
+        const int64_t v = w * 64 + lane;
+        bool d = true;
+        if (v < nv) {
+            const int64_t b = row_off[v], e = row_off[v + 1];
+            d = (e == b) || (e == b + 1 && col[b] == (uint32_t)v);
+        }
+        const unsigned long long m = __ballot(d);
+        if (lane == 0) dead[w] = m;
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_top1(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                              int64_t nv, uint32_t *__restrict__ top1) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
+        const int64_t b = row_off[v];
+        top1[v] = (row_off[v + 1] > b) ? col[b] : (uint32_t)v;
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_popc(const unsigned long long *__restrict__ bm, int64_t nwords,
+                                              unsigned long long *out) {
+    unsigned long long c = 0;
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
+        c += (unsigned long long)__popcll(bm[w]);
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(out, c);
+}
+
 // m_comp (Graph500 TEPS numerator) and reached count, outside the timed region.
 __global__ __launch_bounds__(kBS) void k_mcomp(const int32_t *__restrict__ dist, const uint32_t *__restrict__ tcnt,
                                                int64_t nv, unsigned long long *out) {
@@ -352,6 +579,22 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipHostMalloc(&ws->h_ring, sizeof(LevelCounters), hipHostMallocDefault));
     BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(unsigned long long)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
+    BFSX_HIP_TRY(hipMalloc(&ws->top1, nv * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_top1, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, g->ctx->stream,
+                       g->d_row_off, g->d_col, g->nv, ws->top1);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipMalloc(&ws->dead, ws->nwords * sizeof(unsigned long long)));
+    hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0,
+                       g->ctx->stream, g->d_row_off, g->d_col, g->nv, ws->nwords, ws->dead);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(unsigned long long), g->ctx->stream));
+    hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, g->ctx->stream,
+                       ws->dead, ws->nwords, ws->d_red);
+    BFSX_HIP_TRY(hipGetLastError());
+    unsigned long long nd = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, g->ctx->stream));
+    BFSX_HIP_TRY(hipStreamSynchronize(g->ctx->stream));
+    ws->n_dead = (int64_t)nd - (ws->nwords * 64 - g->nv); // minus padding bits
     return BFSX_OK;
 }
 
@@ -360,7 +603,7 @@ int ws_alloc(bfsx_graph *g) {
 void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
     for (void *p : {(void *)ws->dist, (void *)ws->parent, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
-                    (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->ring, (void *)ws->d_red})
+                    (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->ring, (void *)ws->d_red, (void *)ws->dead, (void *)ws->top1})
         if (p) (void)hipFree(p);
     if (ws->h_ring) (void)hipHostFree(ws->h_ring);
     if (ws->ev_start) (void)hipEventDestroy(ws->ev_start);
@@ -382,10 +625,13 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     const int64_t nv = g->nv, nwords = ws->nwords;
     const unsigned cap = (unsigned)ctx->num_cus * 8u;
 
+    int64_t src_off[2];
+    BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
+
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ws->dist, 0x7FFFFFFF, (size_t)nv, st));
-    BFSX_HIP_TRY(hipMemsetAsync(ws->vis, 0, nwords * sizeof(unsigned long long), st));
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, nwords * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
     BFSX_HIP_TRY(hipMemsetAsync(ws->ring, 0, 4 * sizeof(LevelCounters), st));
     hipLaunchKernelGGL(k_init_source, dim3(1), dim3(64), 0, st, (uint32_t)source, g->d_row_off, ws->dist,
                        ws->parent, ws->vis, ws->qa, ws->ring);
@@ -394,7 +640,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     bool in_queue = true; // frontier currently held in ws->qa (else in ws->front)
     int64_t nf = 1, prev_nf = 0;
-    int64_t mf = -1;      // unknown for the source frontier (no host sync before level 0)
+    int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded
     int64_t mu = g->nnz;  // Beamer m_u: adjacency entries of unvisited vertices
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
@@ -432,20 +678,29 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             in_queue = true;
         }
         if (dir == BFSX_DIR_TOPDOWN) {
-            hipLaunchKernelGGL(k_td, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, g->d_row_off,
-                               g->d_col, ws->qa, (uint32_t)nf, ws->qb, ws->vis, ws->dist, ws->parent, ws->ring,
-                               level, opt.hub_degree, ws->hubs);
+            const dim3 gtd(clamp_grid((nf + kBS - 1) / kBS, cap));
+            if (opt.agent_probe)
+                hipLaunchKernelGGL(k_td<true>, gtd, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa, (uint32_t)nf,
+                                   ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level, opt.hub_degree, ws->hubs);
+            else
+                hipLaunchKernelGGL(k_td<false>, gtd, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa, (uint32_t)nf,
+                                   ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level, opt.hub_degree, ws->hubs);
             BFSX_HIP_TRY(hipGetLastError());
-            if (mf < 0 || mf > (int64_t)opt.hub_degree) {
-                hipLaunchKernelGGL(k_td_hubs, dim3(cap), dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs, ws->qb,
-                                   ws->vis, ws->dist, ws->parent, ws->ring, level);
+            if (mf > (int64_t)opt.hub_degree) { // some frontier vertex may exceed the hub degree
+                const dim3 gh(clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
+                if (opt.agent_probe)
+                    hipLaunchKernelGGL(k_td_hubs<true>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
+                                       ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level);
+                else
+                    hipLaunchKernelGGL(k_td_hubs<false>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
+                                       ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level);
                 BFSX_HIP_TRY(hipGetLastError());
             }
             td_levels++;
         } else {
-            hipLaunchKernelGGL(k_bu, dim3(clamp_grid((nwords + kWaves - 1) / kWaves, cap)), dim3(kBS), 0, st,
-                               g->d_row_off, g->d_col, ws->front, ws->next, ws->vis, ws->dist, ws->parent,
-                               ws->ring, level, nwords, nv);
+            hipLaunchKernelGGL(k_bu, dim3(clamp_grid((nwords + kWaves * 64 - 1) / (kWaves * 64), cap)), dim3(kBS), 0,
+                               st, g->d_row_off, g->d_col, ws->top1, ws->front, ws->next, ws->vis, ws->dist,
+                               ws->parent, ws->ring, level, nwords, nv);
             BFSX_HIP_TRY(hipGetLastError());
             bu_levels++;
         }
@@ -461,10 +716,11 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         ls.frontier_in = nf;
         ls.frontier_out = nf_new;
         ls.mf_in = mf;
-        ls.unvisited_in = nv - visited;
+        ls.unvisited_in = nv - visited - ws->n_dead; // live candidates (isolated ones are pre-visited)
         ls.scanned = (dir == BFSX_DIR_TOPDOWN) ? mf : (int64_t)ws->h_ring->scanned;
+        ls.claims = (int64_t)ws->h_ring->claims;
         g->level_stats.push_back(ls);
-        if (dir == BFSX_DIR_TOPDOWN) examined += (mf < 0 ? 0 : mf);
+        if (dir == BFSX_DIR_TOPDOWN) examined += mf;
         else examined += (int64_t)ws->h_ring->scanned;
         visited += nf_new;
         mu -= mf_new;
@@ -486,16 +742,6 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         g->level_cum_ms[l] = t;
         g->level_stats[l].cum_ms = t;
         g->level_stats[l].kernel_ms = k;
-    }
-    if (!g->level_stats.empty() && g->level_stats[0].mf_in < 0) {
-        // the source's degree was written by k_init_source into the scratch slot
-        unsigned long long d0 = 0;
-        BFSX_HIP_TRY(hipMemcpy(&d0, &ws->ring[3].pad[0], sizeof(d0), hipMemcpyDeviceToHost));
-        g->level_stats[0].mf_in = (int64_t)d0;
-        if (g->level_stats[0].direction == BFSX_DIR_TOPDOWN) {
-            g->level_stats[0].scanned = (int64_t)d0;
-            examined += (int64_t)d0;
-        }
     }
     g->last_source = source;
     if (stats) {

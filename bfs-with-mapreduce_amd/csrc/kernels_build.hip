@@ -177,8 +177,92 @@ int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t s
     return BFSX_OK;
 }
 
+// Segmented radix sort of every CSR row (keys_in -> keys_out), in row chunks of < 2^31 entries
+// (rocPRIM's segmented sort takes 32-bit sizes).
+template <class K>
+int sort_rows(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz, const K *keys_in, K *keys_out,
+              unsigned end_bit) {
+    if (nnz <= 0) return BFSX_OK;
+    std::vector<int64_t> h_off;
+    const int64_t kChunk = (int64_t)1 << 31;
+    std::vector<int64_t> row_cuts{0};
+    if (nnz >= kChunk) {
+        h_off.resize(nv + 1);
+        BFSX_HIP_TRY(hipMemcpy(h_off.data(), d_off, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        int64_t r = 0;
+        while (r < nv) {
+            const int64_t limit = h_off[r] + kChunk - 1;
+            int64_t r2 = std::upper_bound(h_off.begin() + r, h_off.end(), limit) - h_off.begin() - 1;
+            if (r2 <= r) return fail(BFSX_E_ARG, "a single adjacency row exceeds 2^31 entries");
+            r2 = std::min<int64_t>(r2, nv);
+            row_cuts.push_back(r2);
+            r = r2;
+        }
+    } else {
+        row_cuts.push_back(nv);
+    }
+    DevBuf<char> tmp;
+    size_t tmp_cap = 0;
+    for (size_t c = 0; c + 1 < row_cuts.size(); c++) {
+        const int64_t r0 = row_cuts[c], r1 = row_cuts[c + 1];
+        const int64_t e0 = h_off.empty() ? 0 : h_off[r0];
+        const int64_t e1 = h_off.empty() ? nnz : h_off[r1];
+        if (e1 == e0) continue;
+        auto beg = rocprim::make_transform_iterator(d_off + r0, SubBase{e0});
+        auto end = rocprim::make_transform_iterator(d_off + r0 + 1, SubBase{e0});
+        size_t tmp_bytes = 0;
+        BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, keys_in + e0, keys_out + e0,
+                                                        (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end, 0,
+                                                        end_bit, stream));
+        if (tmp_bytes > tmp_cap) {
+            tmp.reset();
+            BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
+            tmp_cap = tmp_bytes;
+        }
+        BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(tmp.p, tmp_bytes, keys_in + e0, keys_out + e0,
+                                                        (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end, 0,
+                                                        end_bit, stream));
+    }
+    BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    return BFSX_OK;
+}
+
+// Key for the degree-descending row order: (UINT32_MAX - deg(nbr)) << 32 | nbr.
+__global__ __launch_bounds__(kBS) void k_degree_keys(const int64_t *__restrict__ off, const uint32_t *__restrict__ col,
+                                                     int64_t nnz, unsigned long long *__restrict__ keys) {
+    for (int64_t j = (int64_t)blockIdx.x * kBS + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * kBS) {
+        const uint32_t x = col[j];
+        const uint64_t d = (uint64_t)(off[x + 1] - off[x]);
+        const uint64_t dk = d >= 0xFFFFFFFFull ? 0ull : 0xFFFFFFFFull - d;
+        keys[j] = (dk << 32) | x;
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_low32(const unsigned long long *__restrict__ keys, int64_t nnz,
+                                               uint32_t *__restrict__ col) {
+    for (int64_t j = (int64_t)blockIdx.x * kBS + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * kBS)
+        col[j] = (uint32_t)keys[j];
+}
+
+// Re-order every row so that high-degree neighbours come first: a bottom-up probe of an unvisited
+// vertex then tests the neighbour most likely to be in a large frontier first (early exit).
+int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz, uint32_t *d_col) {
+    if (nnz <= 0) return BFSX_OK;
+    DevBuf<unsigned long long> k0, k1;
+    BFSX_HIP_TRY(k0.alloc(nnz));
+    BFSX_HIP_TRY(k1.alloc(nnz));
+    hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(nnz, kBS)), dim3(kBS), 0, stream, d_off, d_col, nnz, k0.p);
+    BFSX_HIP_TRY(hipGetLastError());
+    int rc = sort_rows(stream, d_off, nv, nnz, k0.p, k1.p, 64u);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_low32, dim3(grid_for(nnz, kBS)), dim3(kBS), 0, stream, k1.p, nnz, d_col);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    return BFSX_OK;
+}
+
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
-                     int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out,
+                     bool degree_order, int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out,
                      uint32_t **d_tuple_cnt_out) {
     DevBuf<uint32_t> deg, tcnt;
     DevBuf<int64_t> off;
@@ -221,59 +305,14 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
         BFSX_HIP_TRY(hipStreamSynchronize(stream));
     }
 
-    // K1d: sort every row (segmented radix sort), in row chunks of < 2^31 entries
+    // K1d: sort every row by neighbour id
     DevBuf<uint32_t> col_s;
     BFSX_HIP_TRY(col_s.alloc(nnz_raw));
-    if (nnz_raw > 0) {
+    {
         unsigned end_bit = 1;
         while (end_bit < 32 && (1ULL << end_bit) < (uint64_t)nv) end_bit++;
-        std::vector<int64_t> h_off;
-        const int64_t kChunk = (int64_t)1 << 31;
-        std::vector<int64_t> row_cuts{0};
-        if (nnz_raw >= kChunk) {
-            h_off.resize(nv + 1);
-            BFSX_HIP_TRY(hipMemcpy(h_off.data(), off.p, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-            int64_t r = 0;
-            while (r < nv) {
-                int64_t limit = h_off[r] + kChunk - 1;
-                int64_t r2 = std::upper_bound(h_off.begin() + r, h_off.end(), limit) - h_off.begin() - 1;
-                if (r2 <= r) return fail(BFSX_E_ARG, "a single adjacency row exceeds 2^31 entries");
-                r2 = std::min<int64_t>(r2, nv);
-                row_cuts.push_back(r2);
-                r = r2;
-            }
-        } else {
-            row_cuts.push_back(nv);
-        }
-        DevBuf<char> tmp;
-        size_t tmp_cap = 0;
-        for (size_t c = 0; c + 1 < row_cuts.size(); c++) {
-            int64_t r0 = row_cuts[c], r1 = row_cuts[c + 1];
-            int64_t e0, e1;
-            if (!h_off.empty()) {
-                e0 = h_off[r0];
-                e1 = h_off[r1];
-            } else {
-                e0 = 0;
-                e1 = nnz_raw;
-            }
-            if (e1 == e0) continue;
-            auto beg = rocprim::make_transform_iterator(off.p + r0, SubBase{e0});
-            auto end = rocprim::make_transform_iterator(off.p + r0 + 1, SubBase{e0});
-            size_t tmp_bytes = 0;
-            BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, col.p + e0, col_s.p + e0,
-                                                            (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end,
-                                                            0, end_bit, stream));
-            if (tmp_bytes > tmp_cap) {
-                tmp.reset();
-                BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
-                tmp_cap = tmp_bytes;
-            }
-            BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(tmp.p, tmp_bytes, col.p + e0, col_s.p + e0,
-                                                            (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end,
-                                                            0, end_bit, stream));
-        }
-        BFSX_HIP_TRY(hipStreamSynchronize(stream));
+        int rc = sort_rows(stream, off.p, nv, nnz_raw, col.p, col_s.p, end_bit);
+        if (rc) return rc;
     }
     col.reset(); // unsorted rows are no longer needed
 
@@ -315,6 +354,13 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
     hipLaunchKernelGGL(k_new_off, dim3(grid_for(nv + 1, kBS)), dim3(kBS), 0, stream, off.p, pos.p, nv, noff.p);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    col_s.reset();
+    keep.reset();
+    pos.reset();
+    if (degree_order) {
+        int rc = order_rows_by_degree(stream, noff.p, nv, nnz, col_f.p);
+        if (rc) return rc;
+    }
 
     *d_row_off_out = noff.release();
     *d_col_out = col_f.release();

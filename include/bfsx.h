@@ -75,6 +75,7 @@ typedef struct bfsx_level_stat {
     int64_t mf_in;         /* sum of frontier degrees (top-down edges scanned) */
     int64_t unvisited_in;  /* WHITE vertices before the pass (bottom-up candidates) */
     int64_t scanned;       /* adjacency entries read (top-down: mf_in; bottom-up: counted) */
+    int64_t claims;        /* top-down: atomic visited-bitmap claims attempted (diagnostics) */
     double kernel_ms;      /* device time of this level's kernels (hipEvents around them) */
     double cum_ms;         /* device time since source init, like the reference's Stopwatch */
 } bfsx_level_stat;
@@ -87,7 +88,10 @@ int bfsx_init(int device, bfsx_ctx **out);
 void bfsx_finalize(bfsx_ctx *ctx);
 /* Options (all optional; defaults preserve reference behaviour):
  *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 14) ; "beta" = int (default 24)
- *   "hub_degree" = int (top-down multi-workgroup bin threshold, default 4096) */
+ *   "hub_degree" = int (top-down multi-workgroup bin threshold, default 64)
+ *   "td_probe" = plain|agent (top-down visited probe load flavour, default plain)
+ *   "row_order" = degree|id (adjacency order inside a CSR row for graphs built afterwards; default
+ *                 degree = high-degree neighbours first, which shortens bottom-up probes) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */
@@ -116,7 +120,8 @@ void bfsx_graph_free(bfsx_graph *g);
 int64_t bfsx_graph_nv(const bfsx_graph *g);  /* vertices */
 int64_t bfsx_graph_nnz(const bfsx_graph *g); /* directed adjacency entries after dedup */
 int64_t bfsx_graph_m(const bfsx_graph *g);   /* input tuples */
-/* D2H copy of the CSR: row_off[nv+1], col[nnz] (either may be NULL). Rows sorted ascending. */
+/* D2H copy of the CSR: row_off[nv+1], col[nnz] (either may be NULL).  Each row holds one
+ * neighbour set; its order follows the "row_order" option the graph was built with. */
 int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col);
 /* Graph500 root sampling: count distinct vertices with a non-self-loop neighbour, seeded. */
 int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots);

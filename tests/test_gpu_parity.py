@@ -20,6 +20,17 @@ def read_dist(name):
         return np.array([int(line.split()[1]) for line in f], dtype=np.int32)
 
 
+def sort_rows(off, col):
+    """Rows sorted ascending (device rows may be degree-ordered; the oracle validator bisects)."""
+    rows = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off))
+    return col[np.lexsort((col, rows))]
+
+
+def same_sets(off, col, goff, gcol):
+    """CSR equality as neighbour sets."""
+    return np.array_equal(goff, off) and np.array_equal(sort_rows(goff, gcol), col)
+
+
 def check_against_oracle(g, nv, off, col, src, u=None, v=None, mr=True):
     dist, parent, st = g.bfs(src)
     if mr:
@@ -48,7 +59,7 @@ def test_reference_test_sets_bit_exact(ctx, name, direction):
         with ctx.load_algs4(path) as g:
             assert g.nv == nv and g.m == len(u) and g.nnz == off[-1]
             goff, gcol = g.csr()
-            assert np.array_equal(goff, off) and np.array_equal(gcol, col)
+            assert same_sets(off, col, goff, gcol)
             dist, parent, st = check_against_oracle(g, nv, off, col, 0, u, v)
             assert np.array_equal(dist, read_dist(name + ".dist"))
             assert O.dist_sha256(dist) == O.dist_sha256(read_dist(name + ".dist"))
@@ -101,7 +112,7 @@ def test_edge_cases_bit_exact(ctx, case, direction):
     try:
         with ctx.from_edges(nv, u, v) as g:
             goff, gcol = g.csr()
-            assert np.array_equal(goff, off) and np.array_equal(gcol, col)
+            assert same_sets(off, col, goff, gcol)
             srcs = {0, nv - 1, nv // 2}
             for s in sorted(srcs):
                 check_against_oracle(g, nv, off, col, s, u, v, mr=(nv <= 3000))
@@ -125,7 +136,7 @@ def test_hub_threshold_sweep(ctx):
                 assert np.array_equal(d, ref)
                 assert O.validate(nv, off, col, 0, d, p) == 0
     finally:
-        ctx.set_option("hub_degree", 4096)
+        ctx.set_option("hub_degree", 64)
         ctx.set_option("direction", "auto")
 
 
@@ -144,7 +155,7 @@ def test_kronecker_bfs_parity(ctx, scale):
     off, col = O.build_sets(nv, ou, ov)
     with ctx.kronecker(scale, 16, seed) as g:
         goff, gcol = g.csr()
-        assert np.array_equal(goff, off) and np.array_equal(gcol, col)
+        assert same_sets(off, col, goff, gcol)
         roots = g.sample_roots(8, seed=3)
         assert len(set(roots.tolist())) == 8
         for r in roots:
@@ -154,12 +165,37 @@ def test_kronecker_bfs_parity(ctx, scale):
         assert len(dirs) > 0
 
 
+@pytest.mark.parametrize("order", ["id", "degree"])
+def test_row_order_option(ctx, order):
+    """Rows in id order are sorted ascending; both orders give identical distances."""
+    seed, scale = 77, 12
+    ou, ov = O.kronecker(scale, 16, seed)
+    nv = 1 << scale
+    off, col = O.build_sets(nv, ou, ov)
+    ctx.set_option("row_order", order)
+    try:
+        with ctx.kronecker(scale, 16, seed) as g:
+            goff, gcol = g.csr()
+            if order == "id":
+                assert np.array_equal(gcol, col)
+            else:
+                assert same_sets(off, col, goff, gcol)
+                deg = np.diff(off)
+                for x in range(0, nv, 97):  # non-increasing neighbour degree inside a row
+                    assert np.all(np.diff(deg[gcol[goff[x]:goff[x + 1]]]) <= 0)
+            r = int(g.sample_roots(1, seed=9)[0])
+            check_against_oracle(g, nv, off, col, r, ou, ov)
+    finally:
+        ctx.set_option("row_order", "degree")
+
+
 def test_kronecker_scale20_validated(ctx):
     """Full-size-style property check: Graph500 validation + oracle distances at scale 20."""
     scale = 20
     with ctx.kronecker(scale, 16, 0x5EED2026) as g:
         nv = g.nv
         off, col = g.csr()
+        col = sort_rows(off, col)
         for r in g.sample_roots(4, seed=11):
             d, p, st = g.bfs(int(r))
             ref, _ = O.csr_bfs(nv, off, col, int(r))
