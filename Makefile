@@ -15,7 +15,7 @@ KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip
 HOST_SRCS   := $(CSRC)/bfsx_api.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 
-all: $(PKG)/libbfsx.so oracle
+all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/bfsx_internal.h include/bfsx.h
 	@mkdir -p $(OBJDIR)
@@ -27,6 +27,9 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h include/bfsx.h
 
 $(PKG)/libbfsx.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+$(PKG)/bfsx_spark: $(HOSTSRC)/bfsx_spark.cpp include/bfsx.h $(PKG)/libbfsx.so
+	$(CXX) $(CXXFLAGS) -o $@ $(HOSTSRC)/bfsx_spark.cpp -L$(PKG) -lbfsx -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -C oracle

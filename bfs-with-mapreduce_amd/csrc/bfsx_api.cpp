@@ -228,12 +228,6 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "row_order must be degree|id");
         return BFSX_OK;
     }
-    if (k == "td_probe") {
-        if (v == "plain") ctx->opt.agent_probe = false;
-        else if (v == "agent") ctx->opt.agent_probe = true;
-        else return fail(BFSX_E_ARG, "td_probe must be plain|agent");
-        return BFSX_OK;
-    }
     if (k == "alpha") return as_int(ctx->opt.alpha);
     if (k == "beta") return as_int(ctx->opt.beta);
     if (k == "hub_degree") {

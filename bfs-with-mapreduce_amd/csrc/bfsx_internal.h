@@ -22,27 +22,12 @@ int fail(int code, const std::string &msg);
                                 std::string(#call) + ": " + hipGetErrorString(e_));          \
     } while (0)
 
-// One 64-byte slot of the per-level counter ring (3 slots, see DESIGN.md "Level loop").
-// Level L reads slot L%3 (its own frontier, already on the host), accumulates the frontier it
-// produces into slot (L+1)%3 and zeroes slot (L+2)%3 -- so no per-level memset is needed.
-struct alignas(64) LevelCounters {
-    unsigned long long nf;   // vertices in the produced frontier
-    unsigned long long mf;   // sum of their degrees (Beamer m_f)
-    unsigned long long nhub; // top-down: frontier vertices deferred to the multi-workgroup bin
-    unsigned long long aux;  // scratch (bitmap->queue compaction cursor)
-    unsigned long long scanned; // bottom-up: adjacency entries read (algorithmic-bytes accounting)
-    unsigned long long claims;  // top-down: atomicOr claims attempted (diagnostics)
-    unsigned long long pad[2];
-};
-static_assert(sizeof(LevelCounters) == 64, "counter slot must be one 64-B line");
-
 struct Options {
     int direction = BFSX_DIR_AUTO;
-    int alpha = 14;            // top-down -> bottom-up when m_f > m_u / alpha
-    int beta = 24;             // bottom-up -> top-down when n_f < n / beta (and shrinking)
+    int alpha = 30;             // top-down -> bottom-up when m_f > m_u / alpha (tuned on scale 26)
+    int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
-    bool agent_probe = false;   // top-down visited probe: agent-scope (L1-bypassing) load vs plain
 };
 
 // ---- kernels_build.hip -------------------------------------------------------------------

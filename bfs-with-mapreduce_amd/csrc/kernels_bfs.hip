@@ -1,16 +1,16 @@
 // kernels_bfs.hip -- the BFS hot path on the GPU (gfx950, wave64).
 //
 // Replaces the reference's per-level Spark job (BfsSpark.java:61-118):
-//   mapper   (:66-87)  GRAY u emits (n, d+1) for n in N(u)          -> K3 top-down push  (k_td, k_td_hubs)
+//   mapper   (:66-87)  GRAY u emits (n, d+1) for n in N(u)          -> K3 top-down push (k_td, k_td_hubs)
 //   reducer  (:90-108) min distance / darkest colour per vertex id  -> fused: atomicOr claim on the
 //                      visited bitmap; the single winner writes dist = level+1 (every contender of a
 //                      level carries the same level+1, so the min is race-free and exact)
-//   collect + contains("GRAY") (:110-117)                            -> K4 frontier count in a device
-//                      counter ring, read back as one 64-B D2H per level
+//   collect + contains("GRAY") (:110-117)                            -> K4 frontier count in a sharded
+//                      device counter slot, read back as one small D2H per level
 //   (no reference analogue)                                          -> K5 bottom-up pull (k_bu) with
 //                      Beamer's direction-optimising switch
-// State: dist int32[n] (INT32_MAX = WHITE), parent int32[n], visited bitmap u64[n/64] (BLACK|GRAY),
-// frontier as a queue u32[] (top-down) or bitmap u64[] (bottom-up).
+// State: dist int32[n] (INT32_MAX = WHITE), parent int32[n], visited bitmap u64[n/64] (BLACK|GRAY,
+// pre-set for isolated vertices), frontier as a queue u32[] (top-down) or a bitmap u64[] (bottom-up).
 #include <algorithm>
 #include <chrono>
 
@@ -18,25 +18,51 @@
 
 namespace bfsx {
 
+namespace {
+
+constexpr int kBS = 256;
+constexpr int kWaves = kBS / 64;
+constexpr int kShards = 64; // stat counters are spread over 64 lines: a single device-scope counter hit
+                            // by every workgroup costs ~12 ns per arrival (MI355X_MICROARCH fan-in row)
+
+struct alignas(64) StatShard {
+    unsigned long long nf;      // vertices in the produced frontier (bottom-up)
+    unsigned long long mf;      // sum of their degrees (Beamer m_f)
+    unsigned long long scanned; // adjacency entries read (bottom-up; algorithmic-bytes accounting)
+    unsigned long long claims;  // top-down atomicOr claims attempted (diagnostics)
+    unsigned long long pad[4];
+};
+
+// Counters of one level.  Level L reads slot L%3 (its own frontier, already on the host), accumulates
+// the frontier it produces into slot (L+1)%3 and zeroes slot (L+2)%3: no per-level memset.
+struct LevelSlot {
+    unsigned long long qtail; // top-down next-queue allocation cursor (= frontier size produced)
+    unsigned long long nhub;  // top-down hub-list length
+    unsigned long long pad[6];
+    StatShard sh[kShards];
+};
+constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(unsigned long long));
+
+} // namespace
+
 struct BfsWorkspace {
     int64_t nv = 0, nwords = 0;
     int32_t *dist = nullptr, *parent = nullptr;
     unsigned long long *vis = nullptr, *front = nullptr, *next = nullptr;
     unsigned long long *dead = nullptr; // isolated vertices + padding (initial visited bitmap)
-    uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex
     int64_t n_dead = 0;                 // isolated vertices (excluding padding)
+    uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
-    LevelCounters *ring = nullptr;   // device, 4 slots (3 ring + 1 scratch)
-    LevelCounters *h_ring = nullptr; // pinned host mirror of one slot
-    unsigned long long *d_red = nullptr; // reductions (m_comp, reached)
-    hipEvent_t ev_start = nullptr;
+    LevelSlot *ring = nullptr;          // device, 3 slots
+    LevelSlot *h_slot = nullptr;        // pinned host mirror of one slot
+    unsigned long long *d_cursor = nullptr; // bitmap -> queue compaction cursor
+    unsigned long long *d_red = nullptr;    // reductions (m_comp, reached)
+    int64_t prev_source = -1;
+    hipEvent_t ev_start = nullptr, ev_end = nullptr;
     std::vector<hipEvent_t> ev_begin, ev_level; // per level: before / after its kernels
 };
 
 namespace {
-
-constexpr int kBS = 256;
-constexpr int kWaves = kBS / 64;
 
 __device__ inline unsigned lane_id() { return threadIdx.x & 63u; }
 
@@ -56,35 +82,64 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
     return x;
 }
 
-__device__ inline void zero_slot(LevelCounters *ring, int level) {
-    if (blockIdx.x == 0 && threadIdx.x < 8)
-        reinterpret_cast<unsigned long long *>(ring + (level + 2) % 3)[threadIdx.x] = 0ull;
+__device__ inline void zero_slot(LevelSlot *ring, int level) {
+    if (blockIdx.x == 0) {
+        unsigned long long *p = reinterpret_cast<unsigned long long *>(ring + (level + 2) % 3);
+        for (int i = threadIdx.x; i < kSlotWords; i += kBS) p[i] = 0ull;
+    }
 }
 
-// ---- K2: source init (after memsets of dist / visited / counters) ------------------------------
-__global__ void k_init_source(uint32_t s, const int64_t *__restrict__ row_off, int32_t *dist, int32_t *parent,
-                              unsigned long long *vis, uint32_t *q, LevelCounters *ring) {
+// Block-uniform: reduce four per-thread values over the workgroup, lane 0 of wave 0 adds them to
+// this workgroup's shard of the level's counters.
+__device__ inline void shard_add(LevelSlot *slot, unsigned long long nf, unsigned long long mf,
+                                 unsigned long long scanned, unsigned long long claims) {
+    __shared__ unsigned long long s_red[4][kWaves];
+    nf = wave_sum(nf);
+    mf = wave_sum(mf);
+    scanned = wave_sum(scanned);
+    claims = wave_sum(claims);
+    const unsigned wave = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        s_red[0][wave] = nf;
+        s_red[1][wave] = mf;
+        s_red[2][wave] = scanned;
+        s_red[3][wave] = claims;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) t += s_red[threadIdx.x][w];
+        if (t) atomicAdd(reinterpret_cast<unsigned long long *>(&slot->sh[blockIdx.x % kShards]) + threadIdx.x, t);
+    }
+}
+
+// ---- K2: source init (after the visited bitmap is reset to the dead mask) -------------------------
+__global__ void k_init_source(uint32_t s, int64_t prev, const unsigned long long *__restrict__ dead,
+                              int32_t *dist, int32_t *parent, unsigned long long *vis, uint32_t *q,
+                              LevelSlot *ring) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
+        // a previous isolated source is pre-visited (dead mask) so k_finalize never resets it
+        if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) dist[prev] = INT32_MAX;
         dist[s] = 0;
         parent[s] = (int32_t)s;
         vis[s >> 6] |= 1ull << (s & 63u);
         q[0] = s;
-        ring[0].nf = 1;
-        ring[0].mf = (unsigned long long)(row_off[s + 1] - row_off[s]);
     }
+    zero_slot(ring, -2); // slot 0
+    zero_slot(ring, -1); // slot 1
 }
 
 // ---- block-level output queue ------------------------------------------------------------------
 // Winners are appended to an LDS buffer (LDS atomics) and flushed to the global next-frontier queue
-// with ONE global atomic per ~kQCap winners: a single device counter hit by every wave serialises
-// at the memory side (measured 2.4 G edges/s on scale 26 with per-wave appends).
+// with ONE global atomic per flush (~kQCap winners): a single device counter hit by every wave
+// serialises at the memory side (measured 2.4 G edges/s on scale 26 with per-wave appends).
 constexpr int kQCap = 4096;
 
 struct BlockQueue {
     uint32_t buf[kQCap];
     uint32_t n;
     uint32_t gbase;
-    unsigned long long mf[kWaves];
 };
 
 // All 64 lanes of every wave call this (wave-uniform control flow).
@@ -100,10 +155,10 @@ __device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
 }
 
 // Block-uniform: every thread calls after a __syncthreads().
-__device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, LevelCounters *cn) {
+__device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn) {
     const uint32_t n = q.n;
     if (n == 0) return;
-    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(&cn->nf, (unsigned long long)n);
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(&cn->qtail, (unsigned long long)n);
     __syncthreads();
     const uint32_t gb = q.gbase;
     for (uint32_t i = threadIdx.x; i < n; i += kBS) qout[gb + i] = q.buf[i];
@@ -114,21 +169,6 @@ __device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, Leve
 
 __device__ inline void bq_init(BlockQueue &q) {
     if (threadIdx.x == 0) q.n = 0;
-}
-
-// Block-uniform epilogue: flush the queue and add the block's degree sum to m_f.
-__device__ inline void bq_finish(BlockQueue &q, uint32_t *__restrict__ qout, LevelCounters *cn,
-                                 unsigned long long acc_mf) {
-    acc_mf = wave_sum(acc_mf);
-    if (lane_id() == 0) q.mf[threadIdx.x >> 6] = acc_mf;
-    __syncthreads();
-    bq_flush(q, qout, cn);
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-#pragma unroll
-        for (int i = 0; i < kWaves; i++) t += q.mf[i];
-        if (t) atomicAdd(&cn->mf, t);
-    }
 }
 
 // ---- K3: top-down push, degree-binned -----------------------------------------------------------
@@ -144,26 +184,22 @@ __device__ inline void bq_finish(BlockQueue &q, uint32_t *__restrict__ qout, Lev
 constexpr int kItems = 4;
 constexpr int kHubBatch = 1024;
 
-template <bool kAgentProbe>
 __device__ inline bool claim(uint32_t v, unsigned long long *vis, unsigned long long &attempts) {
     const unsigned long long bit = 1ull << (v & 63u);
     unsigned long long *w = vis + (v >> 6);
-    unsigned long long cur;
-    if (kAgentProbe) cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else cur = *w;
-    if (cur & bit) return false; // bits are only ever set: a stale line can only under-report
+    if (*w & bit) return false; // bits are only ever set: a stale line can only under-report
     attempts++;
     return !(atomicOr(w, bit) & bit);
 }
 
-// Sweep `cnt` edges x0..x0+cnt of a segment table (scan/beg/u in LDS, n entries) in steps of
+// Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries) in steps of
 // kBS*kItems.  Block-uniform.
-template <bool kAgentProbe, class ScanT>
+template <class ScanT>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const int64_t *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, unsigned long long *vis,
                                       int32_t *__restrict__ dist, int32_t *__restrict__ parent, int32_t nd,
-                                      BlockQueue &q, uint32_t *__restrict__ qout, LevelCounters *cn,
+                                      BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn,
                                       unsigned long long &acc_mf, unsigned long long &attempts) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
@@ -188,7 +224,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
 #pragma unroll
         for (int k = 0; k < kItems; k++) {
             bool win = false;
-            if (valid[k] && claim<kAgentProbe>(v[k], vis, attempts)) {
+            if (valid[k] && claim(v[k], vis, attempts)) {
                 win = true;
                 dist[v[k]] = nd;
                 parent[v[k]] = (int32_t)pu[k];
@@ -201,19 +237,13 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
     }
 }
 
-__device__ inline void add_attempts(LevelCounters *cn, unsigned long long attempts) {
-    attempts = wave_sum(attempts);
-    if (lane_id() == 0 && attempts) atomicAdd(&cn->claims, attempts);
-}
-
-template <bool kAgentProbe>
 __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, unsigned long long *vis,
                                             int32_t *__restrict__ dist, int32_t *__restrict__ parent,
-                                            LevelCounters *ring, int level, uint32_t hub_deg,
+                                            LevelSlot *ring, int level, uint32_t hub_deg,
                                             uint32_t *__restrict__ hubs) {
-    LevelCounters *cn = ring + (level + 1) % 3;
+    LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
     __shared__ int64_t s_beg[kBS];
@@ -253,21 +283,20 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
         s_u[tid] = u;
         if (tid == 0) s_scan[kBS] = total;
         __syncthreads();
-        sweep_segments<kAgentProbe>(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, dist, parent, nd, q, qout,
-                                    cn, acc_mf, attempts);
+        sweep_segments(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, dist, parent, nd, q, qout, cn,
+                       acc_mf, attempts);
         __syncthreads();
     }
-    add_attempts(cn, attempts);
-    bq_finish(q, qout, cn, acc_mf);
+    bq_flush(q, qout, cn);
+    shard_add(cn, 0, acc_mf, 0, attempts);
 }
 
-template <bool kAgentProbe>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row_off,
                                                  const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  unsigned long long *vis, int32_t *__restrict__ dist,
-                                                 int32_t *__restrict__ parent, LevelCounters *ring, int level) {
-    LevelCounters *cn = ring + (level + 1) % 3;
+                                                 int32_t *__restrict__ parent, LevelSlot *ring, int level) {
+    LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ unsigned long long s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
@@ -299,7 +328,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row
         }
         s_tsum[tid] = local;
         __syncthreads();
-        // block exclusive scan of the per-thread sums (256 entries, Hillis-Steele in LDS)
+        // block inclusive scan of the per-thread sums (Hillis-Steele in LDS)
         for (int off = 1; off < kBS; off <<= 1) {
             const unsigned long long add = tid >= (unsigned)off ? s_tsum[tid - off] : 0ull;
             __syncthreads();
@@ -311,19 +340,19 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int idx = (int)tid * kPer + k;
-            if (idx < kHubBatch) s_scan[idx] = (idx < hb) ? run : total;
+            s_scan[idx] = (idx < hb) ? run : total;
             run += d[k];
         }
         if (tid == 0) s_scan[kHubBatch] = total;
         __syncthreads();
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
-        sweep_segments<kAgentProbe>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, dist, parent, nd,
-                                    q, qout, cn, acc_mf, attempts);
+        sweep_segments(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, dist, parent, nd, q, qout, cn,
+                       acc_mf, attempts);
         __syncthreads();
     }
-    add_attempts(cn, attempts);
-    bq_finish(q, qout, cn, acc_mf);
+    bq_flush(q, qout, cn);
+    shard_add(cn, 0, acc_mf, 0, attempts);
 }
 
 // ---- K5: bottom-up pull --------------------------------------------------------------------------
@@ -340,8 +369,7 @@ __device__ inline int select_bit(unsigned long long x, int r) { // position of t
     int pos = 0;
 #pragma unroll
     for (int half = 32; half >= 1; half >>= 1) {
-        const unsigned long long lowmask = (half == 64) ? ~0ull : ((1ull << half) - 1ull);
-        const int c = __popcll(x & lowmask);
+        const int c = __popcll(x & ((1ull << half) - 1ull));
         if (r >= c) {
             r -= c;
             x >>= half;
@@ -356,11 +384,10 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
                                             const unsigned long long *__restrict__ front,
                                             unsigned long long *__restrict__ next,
                                             unsigned long long *__restrict__ vis, int32_t *__restrict__ dist,
-                                            int32_t *__restrict__ parent, LevelCounters *ring, int level,
-                                            int64_t nwords, int64_t nv) {
-    LevelCounters *cn = ring + (level + 1) % 3;
+                                            int32_t *__restrict__ parent, LevelSlot *ring, int level,
+                                            int64_t nwords) {
+    LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
-    __shared__ unsigned long long s_nf[kWaves], s_mf[kWaves], s_sc[kWaves];
     __shared__ unsigned long long s_nx[kWaves][64];
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
@@ -382,10 +409,6 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
         __builtin_amdgcn_wave_barrier();
         for (uint32_t t0 = 0; t0 < total; t0 += 64) {
             const uint32_t idx = t0 + lane;
-            bool found = false;
-            uint32_t par = 0;
-            int64_t v = 0;
-            unsigned long long deg = 0, scanned = 0;
             // owning word (largest k with excl[k] <= idx) and bit, computed by every lane (shuffles
             // need all lanes active); lanes past the end work on a clamped index and are masked below
             const uint32_t ic = idx < total ? idx : total - 1;
@@ -398,10 +421,11 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
             const unsigned long long uk = __shfl(unv, k);
             const int bit = select_bit(uk, (int)(ic - __shfl(excl, k)));
             if (idx < total) {
-                v = (w0 + k) * 64 + bit; // < nv: padding bits are set in the dead mask
+                const int64_t v = (w0 + k) * 64 + bit; // < nv: padding bits are set in the dead mask
                 const int64_t b = row_off[v], e = row_off[v + 1];
-                deg = (unsigned long long)(e - b);
                 const uint32_t x = top1[v];
+                bool found = false;
+                uint32_t par = 0;
                 int64_t j = b + 1;
                 if ((front[x >> 6] >> (x & 63u)) & 1ull) {
                     found = true;
@@ -426,16 +450,15 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
                         j += left < 4 ? left : 4;
                     }
                 }
-                scanned = (unsigned long long)(j - b);
+                acc_sc += (unsigned long long)(j - b);
+                if (found) {
+                    dist[v] = nd;
+                    parent[v] = (int32_t)par;
+                    atomicOr(&s_nx[wave][k], 1ull << bit);
+                    acc_mf += (unsigned long long)(e - b);
+                    acc_nf += 1;
+                }
             }
-            if (found) {
-                dist[v] = nd;
-                parent[v] = (int32_t)par;
-                atomicOr(&s_nx[wave][k], 1ull << bit);
-                acc_mf += deg;
-                acc_nf += 1;
-            }
-            acc_sc += scanned;
         }
         __builtin_amdgcn_wave_barrier();
         const unsigned long long nxl = s_nx[wave][lane];
@@ -444,29 +467,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
             if (nxl) vis[wl] = vwl | nxl;
         }
     }
-    acc_nf = wave_sum(acc_nf);
-    acc_mf = wave_sum(acc_mf);
-    acc_sc = wave_sum(acc_sc);
-    if (lane == 0) {
-        s_nf[wave] = acc_nf;
-        s_mf[wave] = acc_mf;
-        s_sc[wave] = acc_sc;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long a = 0, b = 0, c = 0;
-#pragma unroll
-        for (int i = 0; i < kWaves; i++) {
-            a += s_nf[i];
-            b += s_mf[i];
-            c += s_sc[i];
-        }
-        if (a) {
-            atomicAdd(&cn->nf, a);
-            atomicAdd(&cn->mf, b);
-        }
-        if (c) atomicAdd(&cn->scanned, c);
-    }
+    shard_add(cn, acc_nf, acc_mf, acc_sc, 0);
 }
 
 // ---- K4: frontier representation changes -------------------------------------------------------
@@ -478,37 +479,79 @@ __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restr
     }
 }
 
-// Ballot/popcount compaction: each lane owns one bitmap word; a wave prefix of the popcounts gives
-// each lane its write offset; one atomic per wave reserves the wave's range.
+// Ballot/popcount compaction of a bitmap into a queue.  A workgroup owns a contiguous range of words
+// (kCompactWords per thread, coalesced), counts its set bits, scans the per-thread counts in LDS and
+// reserves its output range with ONE atomic; the grid is kept small (<= 256 workgroups) so the
+// reservation counter sees a few hundred arrivals, not one per wave.
+constexpr int kCompactWords = 16;
+
 __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const unsigned long long *__restrict__ bm, int64_t nwords,
-                                                         uint32_t *__restrict__ q, unsigned long long *cursor) {
-    const unsigned lane = lane_id();
-    for (int64_t w0 = (int64_t)blockIdx.x * kBS; w0 < nwords; w0 += (int64_t)gridDim.x * kBS) {
-        const int64_t w = w0 + threadIdx.x;
-        unsigned long long x = (w < nwords) ? bm[w] : 0ull;
-        const uint32_t c = (uint32_t)__popcll(x);
+                                                         int64_t words_per_block, uint32_t *__restrict__ q,
+                                                         unsigned long long *cursor) {
+    __shared__ uint32_t s_wsum[kWaves];
+    __shared__ uint32_t s_base;
+    const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const int64_t wb = (int64_t)blockIdx.x * words_per_block;
+    const int64_t we = min(nwords, wb + words_per_block);
+    for (int64_t w0 = wb; w0 < we; w0 += (int64_t)kBS * kCompactWords) {
+        unsigned long long x[kCompactWords];
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < kCompactWords; i++) {
+            const int64_t w = w0 + (int64_t)i * kBS + tid;
+            x[i] = w < we ? bm[w] : 0ull;
+            c += (uint32_t)__popcll(x[i]);
+        }
         const uint32_t inc = wave_incl_scan(c);
-        const uint32_t tot = __shfl(inc, 63);
-        uint32_t base = 0;
-        if (lane == 63 && tot) base = (uint32_t)atomicAdd(cursor, (unsigned long long)tot);
-        base = __shfl(base, 63);
-        uint32_t p = base + inc - c;
-        while (x) {
-            const int b = __ffsll((long long)x) - 1;
-            q[p++] = (uint32_t)(w * 64 + b);
-            x &= x - 1ull;
+        if (lane == 63) s_wsum[wave] = inc;
+        __syncthreads();
+        uint32_t woff = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) {
+            woff += (w < (int)wave) ? s_wsum[w] : 0u;
+            total += s_wsum[w];
+        }
+        if (tid == 0) s_base = total ? (uint32_t)atomicAdd(cursor, (unsigned long long)total) : 0u;
+        __syncthreads();
+        uint32_t p = s_base + woff + inc - c;
+#pragma unroll
+        for (int i = 0; i < kCompactWords; i++) {
+            unsigned long long y = x[i];
+            const int64_t w = w0 + (int64_t)i * kBS + tid;
+            while (y) {
+                const int b = __ffsll((long long)y) - 1;
+                q[p++] = (uint32_t)(w * 64 + b);
+                y &= y - 1ull;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// After the last level: vertices left unvisited in this BFS (and not isolated) get INT32_MAX, so the
+// per-BFS init never has to rewrite the whole distance array (isolated vertices keep the INT32_MAX
+// written once when the workspace is created).
+__global__ __launch_bounds__(kBS) void k_finalize(const unsigned long long *__restrict__ vis, int64_t nwords,
+                                                  int32_t *__restrict__ dist) {
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
+        unsigned long long u = ~vis[w];
+        while (u) {
+            const int b = __ffsll((long long)u) - 1;
+            dist[w * 64 + b] = INT32_MAX;
+            u &= u - 1ull;
         }
     }
 }
 
 // Dead mask: vertices that no BFS can reach from elsewhere (degree 0, or a self-loop only) plus the
 // padding bits of the last word.  The visited bitmap starts as this mask, so bottom-up waves skip
-// words that hold only visited/isolated vertices with one uniform branch.
+// groups that hold only visited/isolated vertices with one uniform branch.
 __global__ __launch_bounds__(kBS) void k_dead_mask(const int64_t *__restrict__ row_off,
                                                    const uint32_t *__restrict__ col, int64_t nv, int64_t nwords,
                                                    unsigned long long *__restrict__ dead) {
     const unsigned lane = lane_id();
-    for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords; w += ((int64_t)gridDim.x * kBS) >> 6) {
+    for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords;
+         w += ((int64_t)gridDim.x * kBS) >> 6) {
         const int64_t v = w * 64 + lane;
         bool d = true;
         if (v < nv) {
@@ -564,6 +607,7 @@ int ws_alloc(bfsx_graph *g) {
     if (g->ws) return BFSX_OK;
     auto *ws = new BfsWorkspace();
     g->ws = ws;
+    hipStream_t st = g->ctx->stream;
     ws->nv = g->nv;
     ws->nwords = (g->nv + 63) / 64;
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
@@ -572,28 +616,31 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(unsigned long long)));
     BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(unsigned long long)));
     BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(unsigned long long)));
+    BFSX_HIP_TRY(hipMalloc(&ws->dead, ws->nwords * sizeof(unsigned long long)));
     BFSX_HIP_TRY(hipMalloc(&ws->qa, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->qb, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->hubs, nv * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ws->ring, 4 * sizeof(LevelCounters)));
-    BFSX_HIP_TRY(hipHostMalloc(&ws->h_ring, sizeof(LevelCounters), hipHostMallocDefault));
+    BFSX_HIP_TRY(hipMalloc(&ws->top1, nv * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&ws->ring, 3 * sizeof(LevelSlot)));
+    BFSX_HIP_TRY(hipHostMalloc(&ws->h_slot, sizeof(LevelSlot), hipHostMallocDefault));
+    BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(unsigned long long)));
     BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(unsigned long long)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
-    BFSX_HIP_TRY(hipMalloc(&ws->top1, nv * sizeof(uint32_t)));
-    hipLaunchKernelGGL(k_top1, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, g->ctx->stream,
-                       g->d_row_off, g->d_col, g->nv, ws->top1);
+    BFSX_HIP_TRY(hipEventCreate(&ws->ev_end));
+    BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ws->dist, 0x7FFFFFFF, nv, st));
+    hipLaunchKernelGGL(k_top1, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, g->d_row_off,
+                       g->d_col, g->nv, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipMalloc(&ws->dead, ws->nwords * sizeof(unsigned long long)));
-    hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0,
-                       g->ctx->stream, g->d_row_off, g->d_col, g->nv, ws->nwords, ws->dead);
+    hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
+                       g->d_row_off, g->d_col, g->nv, ws->nwords, ws->dead);
     BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(unsigned long long), g->ctx->stream));
-    hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, g->ctx->stream,
-                       ws->dead, ws->nwords, ws->d_red);
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
+                       ws->nwords, ws->d_red);
     BFSX_HIP_TRY(hipGetLastError());
     unsigned long long nd = 0;
-    BFSX_HIP_TRY(hipMemcpyAsync(&nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, g->ctx->stream));
-    BFSX_HIP_TRY(hipStreamSynchronize(g->ctx->stream));
+    BFSX_HIP_TRY(hipMemcpyAsync(&nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
     ws->n_dead = (int64_t)nd - (ws->nwords * 64 - g->nv); // minus padding bits
     return BFSX_OK;
 }
@@ -603,10 +650,12 @@ int ws_alloc(bfsx_graph *g) {
 void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
     for (void *p : {(void *)ws->dist, (void *)ws->parent, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
-                    (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->ring, (void *)ws->d_red, (void *)ws->dead, (void *)ws->top1})
+                    (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
+                    (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red})
         if (p) (void)hipFree(p);
-    if (ws->h_ring) (void)hipHostFree(ws->h_ring);
+    if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->ev_start) (void)hipEventDestroy(ws->ev_start);
+    if (ws->ev_end) (void)hipEventDestroy(ws->ev_end);
     for (auto e : ws->ev_level) (void)hipEventDestroy(e);
     for (auto e : ws->ev_begin) (void)hipEventDestroy(e);
     delete ws;
@@ -630,18 +679,17 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
 
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
-    BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ws->dist, 0x7FFFFFFF, (size_t)nv, st));
     BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, nwords * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
-    BFSX_HIP_TRY(hipMemsetAsync(ws->ring, 0, 4 * sizeof(LevelCounters), st));
-    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(64), 0, st, (uint32_t)source, g->d_row_off, ws->dist,
-                       ws->parent, ws->vis, ws->qa, ws->ring);
+    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, (uint32_t)source, ws->prev_source, ws->dead,
+                       ws->dist, ws->parent, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
+    ws->prev_source = source;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     bool in_queue = true; // frontier currently held in ws->qa (else in ws->front)
     int64_t nf = 1, prev_nf = 0;
     int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded
-    int64_t mu = g->nnz;  // Beamer m_u: adjacency entries of unvisited vertices
+    int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
     g->level_dirs.clear();
@@ -671,45 +719,47 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue) {
-            BFSX_HIP_TRY(hipMemsetAsync(&ws->ring[3].aux, 0, sizeof(unsigned long long), st));
-            hipLaunchKernelGGL(k_bitmap_to_queue, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0,
-                               st, ws->front, nwords, ws->qa, &ws->ring[3].aux);
+            BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(unsigned long long), st));
+            const int64_t per_block_min = (int64_t)kBS * kCompactWords;
+            const unsigned gb = clamp_grid((nwords + per_block_min - 1) / per_block_min, 256);
+            const int64_t wpb = ((nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
+            hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, nwords, wpb, ws->qa,
+                               ws->d_cursor);
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = true;
         }
         if (dir == BFSX_DIR_TOPDOWN) {
-            const dim3 gtd(clamp_grid((nf + kBS - 1) / kBS, cap));
-            if (opt.agent_probe)
-                hipLaunchKernelGGL(k_td<true>, gtd, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa, (uint32_t)nf,
-                                   ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level, opt.hub_degree, ws->hubs);
-            else
-                hipLaunchKernelGGL(k_td<false>, gtd, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa, (uint32_t)nf,
-                                   ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level, opt.hub_degree, ws->hubs);
+            hipLaunchKernelGGL(k_td, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, g->d_row_off,
+                               g->d_col, ws->qa, (uint32_t)nf, ws->qb, ws->vis, ws->dist, ws->parent, ws->ring,
+                               level, opt.hub_degree, ws->hubs);
             BFSX_HIP_TRY(hipGetLastError());
             if (mf > (int64_t)opt.hub_degree) { // some frontier vertex may exceed the hub degree
                 const dim3 gh(clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
-                if (opt.agent_probe)
-                    hipLaunchKernelGGL(k_td_hubs<true>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                                       ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level);
-                else
-                    hipLaunchKernelGGL(k_td_hubs<false>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                                       ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level);
+                hipLaunchKernelGGL(k_td_hubs, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs, ws->qb,
+                                   ws->vis, ws->dist, ws->parent, ws->ring, level);
                 BFSX_HIP_TRY(hipGetLastError());
             }
             td_levels++;
         } else {
             hipLaunchKernelGGL(k_bu, dim3(clamp_grid((nwords + kWaves * 64 - 1) / (kWaves * 64), cap)), dim3(kBS), 0,
                                st, g->d_row_off, g->d_col, ws->top1, ws->front, ws->next, ws->vis, ws->dist,
-                               ws->parent, ws->ring, level, nwords, nv);
+                               ws->parent, ws->ring, level, nwords);
             BFSX_HIP_TRY(hipGetLastError());
             bu_levels++;
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-        BFSX_HIP_TRY(hipMemcpyAsync(ws->h_ring, ws->ring + (level + 1) % 3, sizeof(LevelCounters),
-                                    hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipMemcpyAsync(ws->h_slot, ws->ring + (level + 1) % 3, sizeof(LevelSlot), hipMemcpyDeviceToHost,
+                                    st));
         BFSX_HIP_TRY(hipStreamSynchronize(st));
+        int64_t s_nf = 0, s_mf = 0, s_sc = 0, s_cl = 0;
+        for (int i = 0; i < kShards; i++) {
+            s_nf += (int64_t)ws->h_slot->sh[i].nf;
+            s_mf += (int64_t)ws->h_slot->sh[i].mf;
+            s_sc += (int64_t)ws->h_slot->sh[i].scanned;
+            s_cl += (int64_t)ws->h_slot->sh[i].claims;
+        }
+        const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? (int64_t)ws->h_slot->qtail : s_nf;
         g->level_dirs.push_back(dir);
-        const int64_t nf_new = (int64_t)ws->h_ring->nf, mf_new = (int64_t)ws->h_ring->mf;
         bfsx_level_stat ls{};
         ls.direction = dir;
         ls.level = level;
@@ -717,23 +767,28 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         ls.frontier_out = nf_new;
         ls.mf_in = mf;
         ls.unvisited_in = nv - visited - ws->n_dead; // live candidates (isolated ones are pre-visited)
-        ls.scanned = (dir == BFSX_DIR_TOPDOWN) ? mf : (int64_t)ws->h_ring->scanned;
-        ls.claims = (int64_t)ws->h_ring->claims;
+        ls.scanned = (dir == BFSX_DIR_TOPDOWN) ? mf : s_sc;
+        ls.claims = s_cl;
         g->level_stats.push_back(ls);
-        if (dir == BFSX_DIR_TOPDOWN) examined += mf;
-        else examined += (int64_t)ws->h_ring->scanned;
+        examined += ls.scanned;
         visited += nf_new;
-        mu -= mf_new;
+        mu -= s_mf;
         prev_nf = nf;
         nf = nf_new;
-        mf = mf_new;
+        mf = s_mf;
         if (dir == BFSX_DIR_TOPDOWN) std::swap(ws->qa, ws->qb);
         else std::swap(ws->front, ws->next);
         if (nf == 0) break;
     }
+    // unvisited (non-isolated) vertices -> INT32_MAX; inside the timed region
+    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis,
+                       nwords, ws->dist);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
+    BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
     const int levels = level + 1;
     float ms = 0.f;
-    BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_level[level]));
+    BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
     g->level_cum_ms.resize(levels);
     for (int l = 0; l < levels; l++) {
         float t = 0.f, k = 0.f;

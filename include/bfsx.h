@@ -87,9 +87,8 @@ const char *bfsx_last_error(void);
 int bfsx_init(int device, bfsx_ctx **out);
 void bfsx_finalize(bfsx_ctx *ctx);
 /* Options (all optional; defaults preserve reference behaviour):
- *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 14) ; "beta" = int (default 24)
+ *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 30) ; "beta" = int (default 24)
  *   "hub_degree" = int (top-down multi-workgroup bin threshold, default 64)
- *   "td_probe" = plain|agent (top-down visited probe load flavour, default plain)
  *   "row_order" = degree|id (adjacency order inside a CSR row for graphs built afterwards; default
  *                 degree = high-degree neighbours first, which shortens bottom-up probes) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
