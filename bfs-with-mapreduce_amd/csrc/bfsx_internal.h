@@ -33,9 +33,11 @@ struct Options {
 // ---- kernels_build.hip -------------------------------------------------------------------
 // Builds the CSR (sorted, de-duplicated neighbour sets, self-loops kept once) from device tuple
 // arrays.  Takes ownership of nothing; d_u/d_v stay owned by the caller.
+// Rows are built for the global id range [lo, lo + nv) only (lo = 0, nv = all for one device);
+// nv_global sizes the sort keys and the degree table of the degree-ordered rows.
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
                      bool degree_order, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
-                     uint32_t **d_tuple_cnt);
+                     uint32_t **d_tuple_cnt, int64_t lo = 0, int64_t nv_global = -1);
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v);
 
@@ -44,6 +46,15 @@ struct BfsWorkspace;
 int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
+// multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
+int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local);
+int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue);
+int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, int64_t *send_counts);
+int dist_td_claim(bfsx_graph *g, const unsigned long long *d_recv, int64_t n);
+int dist_frontier_slice(bfsx_graph *g, unsigned long long *d_slice);
+int dist_bu_step(bfsx_graph *g, const unsigned long long *d_front_global);
+int dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local);
+int dist_finish(bfsx_graph *g);
 void bfs_workspace_free(BfsWorkspace *ws);
 
 } // namespace bfsx
@@ -57,7 +68,11 @@ struct bfsx_ctx {
 
 struct bfsx_graph {
     bfsx_ctx *ctx = nullptr;
-    int64_t nv = 0, nnz = 0, m = 0;
+    int64_t nv = 0, nnz = 0, m = 0; // nv = rows held here (all vertices unless partitioned)
+    // 1-D partition (multi-GPU): this rank holds rows of global ids [v_lo, v_lo + nv); chunk ids per
+    // rank (multiple of 64); adjacency entries are global ids.  Single device: v_lo = 0, nranks = 1.
+    int64_t nv_global = 0, v_lo = 0, chunk = 0;
+    int rank = 0, nranks = 1;
     int64_t *d_row_off = nullptr; // [nv+1]
     uint32_t *d_col = nullptr;    // [nnz]
     uint32_t *d_tuple_cnt = nullptr; // [nv]: input tuples whose first endpoint is v (m_comp)

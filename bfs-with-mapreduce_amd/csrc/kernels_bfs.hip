@@ -13,6 +13,7 @@
 // pre-set for isolated vertices), frontier as a queue u32[] (top-down) or a bitmap u64[] (bottom-up).
 #include <algorithm>
 #include <chrono>
+#include <type_traits>
 
 #include "bfsx_internal.h"
 
@@ -58,6 +59,13 @@ struct BfsWorkspace {
     unsigned long long *d_cursor = nullptr; // bitmap -> queue compaction cursor
     unsigned long long *d_red = nullptr;    // reductions (m_comp, reached)
     int64_t prev_source = -1;
+    // multi-GPU level state (bfsx_dist_*)
+    unsigned long long *remote = nullptr, *sendbuf_tmp = nullptr; // unbucketed remote pairs
+    int64_t remote_cap = 0;
+    unsigned long long *d_dist_ctr = nullptr; // [0] remote tail, [1..kMaxRanks] count, [...] cursor
+    int d_level = 0, d_dir = BFSX_DIR_TOPDOWN;
+    bool d_in_queue = true;
+    int64_t d_nf = 0, d_mf = 0;
     hipEvent_t ev_start = nullptr, ev_end = nullptr;
     std::vector<hipEvent_t> ev_begin, ev_level; // per level: before / after its kernels
 };
@@ -192,15 +200,58 @@ __device__ inline bool claim(uint32_t v, unsigned long long *vis, unsigned long 
     return !(atomicOr(w, bit) & bit);
 }
 
-// Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries) in steps of
-// kBS*kItems.  Block-uniform.
-template <class ScanT>
+// 1-D partition of the vertex ids (multi-GPU path): this rank owns global ids [lo, lo+chunk) and
+// stores their rows; adjacency entries stay global.  Single-GPU graphs use lo = 0, one rank.
+struct Part {
+    uint32_t lo;     // first owned global id
+    uint32_t chunk;  // ids per rank (multiple of 64)
+    uint32_t rank;
+    uint32_t pad;
+    unsigned long long *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
+    unsigned long long *remote_tail; // their allocation cursor
+};
+
+// Remote pairs, LDS-buffered like the local queue (multi-GPU path only).
+constexpr int kRCap = 2048;
+struct RemoteQueue {
+    unsigned long long buf[kRCap];
+    uint32_t n;
+    uint32_t gbase;
+};
+
+__device__ inline void rq_push(RemoteQueue &q, bool send, unsigned long long pair) {
+    const unsigned long long mask = __ballot(send);
+    if (mask == 0) return;
+    const unsigned lane = lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(&q.n, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (send) q.buf[base + __popcll(mask & ((1ull << lane) - 1ull))] = pair;
+}
+
+__device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
+    const uint32_t n = q.n;
+    if (n == 0) return;
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(pt.remote_tail, (unsigned long long)n);
+    __syncthreads();
+    const uint32_t gb = q.gbase;
+    for (uint32_t i = threadIdx.x; i < n; i += kBS) pt.remote[gb + i] = q.buf[i];
+    __syncthreads();
+    if (threadIdx.x == 0) q.n = 0;
+    __syncthreads();
+}
+
+// Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries; u = local row id)
+// in steps of kBS*kItems.  Block-uniform.  kDist: targets owned by another rank become remote pairs.
+template <bool kDist, class ScanT>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const int64_t *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, unsigned long long *vis,
                                       int32_t *__restrict__ dist, int32_t *__restrict__ parent, int32_t nd,
-                                      BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn,
-                                      unsigned long long &acc_mf, unsigned long long &attempts) {
+                                      BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn, const Part &pt,
+                                      RemoteQueue *rq, unsigned long long &acc_mf,
+                                      unsigned long long &attempts) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -218,31 +269,39 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                     else hi = mid - 1;
                 }
                 v[k] = col[s_beg[lo] + (int64_t)(x - (uint64_t)s_scan[lo])];
-                pu[k] = s_u[lo];
+                pu[k] = s_u[lo] + pt.lo; // global id of the frontier vertex
             }
         }
 #pragma unroll
         for (int k = 0; k < kItems; k++) {
-            bool win = false;
-            if (valid[k] && claim(v[k], vis, attempts)) {
-                win = true;
-                dist[v[k]] = nd;
-                parent[v[k]] = (int32_t)pu[k];
-                acc_mf += (unsigned long long)(row_off[v[k] + 1] - row_off[v[k]]);
+            bool win = false, send = false;
+            uint32_t vl = v[k];
+            if (kDist) {
+                send = valid[k] && (v[k] / pt.chunk) != pt.rank;
+                vl = v[k] - pt.lo;
             }
-            bq_push(q, win, v[k]);
+            if (valid[k] && !send && claim(vl, vis, attempts)) {
+                win = true;
+                dist[vl] = nd;
+                parent[vl] = (int32_t)pu[k];
+                acc_mf += (unsigned long long)(row_off[vl + 1] - row_off[vl]);
+            }
+            bq_push(q, win, vl);
+            if (kDist) rq_push(*rq, send, ((unsigned long long)v[k] << 32) | pu[k]);
         }
         __syncthreads();
         if (q.n > (uint32_t)(kQCap - kBS * kItems)) bq_flush(q, qout, cn);
+        if (kDist && rq->n > (uint32_t)(kRCap - kBS * kItems)) rq_flush(*rq, pt);
     }
 }
 
+template <bool kDist>
 __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, unsigned long long *vis,
                                             int32_t *__restrict__ dist, int32_t *__restrict__ parent,
                                             LevelSlot *ring, int level, uint32_t hub_deg,
-                                            uint32_t *__restrict__ hubs) {
+                                            uint32_t *__restrict__ hubs, Part pt) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
@@ -250,7 +309,10 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
     __shared__ uint32_t s_u[kBS];
     __shared__ uint32_t s_wsum[kWaves];
     __shared__ BlockQueue q;
+    __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
+    RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
+    if (kDist && threadIdx.x == 0) rq->n = 0;
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     unsigned long long acc_mf = 0, attempts = 0;
@@ -283,26 +345,31 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
         s_u[tid] = u;
         if (tid == 0) s_scan[kBS] = total;
         __syncthreads();
-        sweep_segments(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, dist, parent, nd, q, qout, cn,
-                       acc_mf, attempts);
+        sweep_segments<kDist>(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, dist, parent, nd, q, qout, cn,
+                              pt, rq, acc_mf, attempts);
         __syncthreads();
     }
     bq_flush(q, qout, cn);
+    if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, 0, attempts);
 }
 
+template <bool kDist>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row_off,
                                                  const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  unsigned long long *vis, int32_t *__restrict__ dist,
-                                                 int32_t *__restrict__ parent, LevelSlot *ring, int level) {
+                                                 int32_t *__restrict__ parent, LevelSlot *ring, int level, Part pt) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ unsigned long long s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
     __shared__ unsigned long long s_tsum[kBS];
     __shared__ BlockQueue q;
+    __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
+    RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
+    if (kDist && threadIdx.x == 0) rq->n = 0;
     const uint32_t nh = (uint32_t)cn->nhub;
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x;
@@ -347,12 +414,97 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row
         __syncthreads();
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
-        sweep_segments(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, dist, parent, nd, q, qout, cn,
-                       acc_mf, attempts);
+        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, dist, parent, nd, q, qout,
+                              cn, pt, rq, acc_mf, attempts);
         __syncthreads();
     }
     bq_flush(q, qout, cn);
+    if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, 0, attempts);
+}
+
+// Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
+__global__ __launch_bounds__(kBS) void k_claim_remote(const unsigned long long *__restrict__ pairs, uint32_t npairs,
+                                                      const int64_t *__restrict__ row_off,
+                                                      unsigned long long *vis, int32_t *__restrict__ dist,
+                                                      int32_t *__restrict__ parent, uint32_t *__restrict__ qout,
+                                                      LevelSlot *ring, int level, uint32_t lo) {
+    LevelSlot *cn = ring + (level + 1) % 3;
+    __shared__ BlockQueue q;
+    bq_init(q);
+    __syncthreads();
+    const int32_t nd = level + 1;
+    unsigned long long acc_mf = 0, attempts = 0;
+    for (uint32_t i0 = blockIdx.x * kBS; i0 < npairs; i0 += gridDim.x * kBS) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool win = false;
+        uint32_t vl = 0;
+        if (i < npairs) {
+            const unsigned long long pr = pairs[i];
+            vl = (uint32_t)(pr >> 32) - lo;
+            if (claim(vl, vis, attempts)) {
+                win = true;
+                dist[vl] = nd;
+                parent[vl] = (int32_t)(uint32_t)pr;
+                acc_mf += (unsigned long long)(row_off[vl + 1] - row_off[vl]);
+            }
+        }
+        bq_push(q, win, vl);
+        __syncthreads();
+        if (q.n > (uint32_t)(kQCap - kBS)) bq_flush(q, qout, cn);
+    }
+    bq_flush(q, qout, cn);
+    shard_add(cn, 0, acc_mf, 0, attempts);
+}
+
+// Multi-GPU: stable bucketing of remote pairs by owning rank (P <= kMaxRanks).  Two passes over the
+// pairs: per-workgroup destination histograms (LDS atomics), then one reservation atomic per
+// (workgroup, destination) and LDS-ranked scatter.
+constexpr int kMaxRanks = 64;
+
+__global__ __launch_bounds__(kBS) void k_bucket_count(const unsigned long long *__restrict__ pairs, uint64_t n,
+                                                      uint32_t chunk, int nranks,
+                                                      unsigned long long *__restrict__ dcount) {
+    __shared__ uint32_t s_h[kMaxRanks];
+    for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS)
+        atomicAdd(&s_h[(uint32_t)(pairs[i] >> 32) / chunk], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < nranks; d += kBS)
+        if (s_h[d]) atomicAdd(&dcount[d], (unsigned long long)s_h[d]);
+}
+
+__global__ __launch_bounds__(kBS) void k_bucket_scatter(const unsigned long long *__restrict__ pairs, uint64_t n,
+                                                        uint32_t chunk, int nranks,
+                                                        const unsigned long long *__restrict__ dcount,
+                                                        unsigned long long *__restrict__ dcursor,
+                                                        unsigned long long *__restrict__ out) {
+    __shared__ uint32_t s_h[kMaxRanks];
+    __shared__ unsigned long long s_base[kMaxRanks];
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kBS; i0 < n; i0 += (uint64_t)gridDim.x * kBS) {
+        for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
+        __syncthreads();
+        const uint64_t i = i0 + threadIdx.x;
+        unsigned long long pr = 0;
+        uint32_t d = 0, r = 0;
+        if (i < n) {
+            pr = pairs[i];
+            d = (uint32_t)(pr >> 32) / chunk;
+            r = atomicAdd(&s_h[d], 1u);
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < nranks; k += kBS) {
+            if (s_h[k]) {
+                unsigned long long off = 0; // exclusive prefix of the destination totals
+                for (int j = 0; j < k; j++) off += dcount[j];
+                s_base[k] = off + atomicAdd(&dcursor[k], (unsigned long long)s_h[k]);
+            }
+        }
+        __syncthreads();
+        if (i < n) out[s_base[d] + r] = pr;
+        __syncthreads();
+    }
 }
 
 // ---- K5: bottom-up pull --------------------------------------------------------------------------
@@ -548,15 +700,15 @@ __global__ __launch_bounds__(kBS) void k_finalize(const unsigned long long *__re
 // groups that hold only visited/isolated vertices with one uniform branch.
 __global__ __launch_bounds__(kBS) void k_dead_mask(const int64_t *__restrict__ row_off,
                                                    const uint32_t *__restrict__ col, int64_t nv, int64_t nwords,
-                                                   unsigned long long *__restrict__ dead) {
+                                                   uint32_t lo, unsigned long long *__restrict__ dead) {
     const unsigned lane = lane_id();
     for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords;
          w += ((int64_t)gridDim.x * kBS) >> 6) {
-        const int64_t v = w * 64 + lane;
+        const int64_t v = w * 64 + lane; // local row id; adjacency entries are global ids
         bool d = true;
         if (v < nv) {
             const int64_t b = row_off[v], e = row_off[v + 1];
-            d = (e == b) || (e == b + 1 && col[b] == (uint32_t)v);
+            d = (e == b) || (e == b + 1 && col[b] == (uint32_t)(v + lo));
         }
         const unsigned long long m = __ballot(d);
         if (lane == 0) dead[w] = m;
@@ -609,7 +761,9 @@ int ws_alloc(bfsx_graph *g) {
     g->ws = ws;
     hipStream_t st = g->ctx->stream;
     ws->nv = g->nv;
-    ws->nwords = (g->nv + 63) / 64;
+    // a partitioned graph pads every rank's slice to chunk/64 words so that frontier slices
+    // all-gather into one global bitmap
+    ws->nwords = g->nranks > 1 ? g->chunk / 64 : (g->nv + 63) / 64;
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
     BFSX_HIP_TRY(hipMalloc(&ws->dist, nv * sizeof(int32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->parent, nv * sizeof(int32_t)));
@@ -632,7 +786,7 @@ int ws_alloc(bfsx_graph *g) {
                        g->d_col, g->nv, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
-                       g->d_row_off, g->d_col, g->nv, ws->nwords, ws->dead);
+                       g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
@@ -651,7 +805,8 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
     for (void *p : {(void *)ws->dist, (void *)ws->parent, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
-                    (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red})
+                    (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
+                    (void *)ws->d_dist_ctr})
         if (p) (void)hipFree(p);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->ev_start) (void)hipEventDestroy(ws->ev_start);
@@ -729,14 +884,15 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             in_queue = true;
         }
         if (dir == BFSX_DIR_TOPDOWN) {
-            hipLaunchKernelGGL(k_td, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, g->d_row_off,
-                               g->d_col, ws->qa, (uint32_t)nf, ws->qb, ws->vis, ws->dist, ws->parent, ws->ring,
-                               level, opt.hub_degree, ws->hubs);
+            const Part pt{};
+            hipLaunchKernelGGL(k_td<false>, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
+                               g->d_row_off, g->d_col, ws->qa, (uint32_t)nf, ws->qb, ws->vis, ws->dist, ws->parent,
+                               ws->ring, level, opt.hub_degree, ws->hubs, pt);
             BFSX_HIP_TRY(hipGetLastError());
             if (mf > (int64_t)opt.hub_degree) { // some frontier vertex may exceed the hub degree
                 const dim3 gh(clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
-                hipLaunchKernelGGL(k_td_hubs, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs, ws->qb,
-                                   ws->vis, ws->dist, ws->parent, ws->ring, level);
+                hipLaunchKernelGGL(k_td_hubs<false>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
+                                   ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level, pt);
                 BFSX_HIP_TRY(hipGetLastError());
             }
             td_levels++;
