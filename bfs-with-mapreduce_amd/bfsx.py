@@ -34,6 +34,10 @@ EXPORTS = [
     "bfsx_graph_nnz", "bfsx_graph_m", "bfsx_graph_csr", "bfsx_sample_roots", "bfsx_bfs",
     "bfsx_result", "bfsx_level_times", "bfsx_level_dirs", "bfsx_level_stats",
     "bfsx_device_synchronize",
+    "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
+    "bfsx_dist_begin", "bfsx_dist_frontier_info", "bfsx_dist_td_expand", "bfsx_dist_td_claim",
+    "bfsx_dist_frontier_slice", "bfsx_dist_bu_step", "bfsx_dist_level_end", "bfsx_dist_finish",
+    "bfsx_dist_mcomp",
 ]
 
 
@@ -98,6 +102,21 @@ def lib():
         L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
         L.bfsx_device_synchronize.argtypes = [_VP]
+        I64P = C.POINTER(C.c_int64)
+        L.bfsx_dist_graph_from_edges.argtypes = [_VP, C.c_int64, _VP, _VP, C.c_int64, C.c_int, C.c_int,
+                                                 C.POINTER(_VP)]
+        L.bfsx_dist_graph_kronecker.argtypes = [_VP, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int, C.POINTER(_VP)]
+        L.bfsx_graph_partition.argtypes = [_VP, I64P, I64P, I64P, I64P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.bfsx_graph_degree.argtypes = [_VP, C.c_int64, I64P]
+        L.bfsx_dist_begin.argtypes = [_VP, C.c_int64, I64P]
+        L.bfsx_dist_frontier_info.argtypes = [_VP, I64P, I64P]
+        L.bfsx_dist_td_expand.argtypes = [_VP, _VP, C.c_int64, _VP]
+        L.bfsx_dist_td_claim.argtypes = [_VP, _VP, C.c_int64]
+        L.bfsx_dist_frontier_slice.argtypes = [_VP, _VP]
+        L.bfsx_dist_bu_step.argtypes = [_VP, _VP]
+        L.bfsx_dist_level_end.argtypes = [_VP, I64P, I64P]
+        L.bfsx_dist_finish.argtypes = [_VP]
+        L.bfsx_dist_mcomp.argtypes = [_VP, I64P, I64P]
         _lib = L
     return _lib
 
@@ -155,6 +174,18 @@ class Context:
     def kronecker(self, scale, edgefactor=16, seed=0x5EED2026):
         g = _VP()
         _check(lib().bfsx_graph_kronecker(self._h, scale, edgefactor, seed, C.byref(g)))
+        return Graph(self, g)
+
+    def dist_from_edges(self, nv, u, v, rank, nranks):
+        u = np.ascontiguousarray(u, dtype=np.uint32)
+        v = np.ascontiguousarray(v, dtype=np.uint32)
+        g = _VP()
+        _check(lib().bfsx_dist_graph_from_edges(self._h, nv, _p(u), _p(v), len(u), rank, nranks, C.byref(g)))
+        return Graph(self, g)
+
+    def dist_kronecker(self, scale, rank, nranks, edgefactor=16, seed=0x5EED2026):
+        g = _VP()
+        _check(lib().bfsx_dist_graph_kronecker(self._h, scale, edgefactor, seed, rank, nranks, C.byref(g)))
         return Graph(self, g)
 
     def kronecker_edges(self, scale, edgefactor=16, seed=0x5EED2026):
@@ -239,6 +270,57 @@ class Graph:
         buf = np.empty(cap, np.int32)
         n = lib().bfsx_level_dirs(self._h, _p(buf), cap)
         return buf[:n].copy()
+
+    def partition(self):
+        a, b, c, d = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        r, p = C.c_int32(), C.c_int32()
+        _check(lib().bfsx_graph_partition(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d), C.byref(r),
+                                          C.byref(p)))
+        return dict(nv_global=a.value, v_lo=b.value, nv_local=c.value, chunk=d.value, rank=r.value,
+                    nranks=p.value)
+
+    def degree(self, v):
+        d = C.c_int64()
+        _check(lib().bfsx_graph_degree(self._h, v, C.byref(d)))
+        return d.value
+
+    # ---- multi-GPU level primitives (device pointers are ints, e.g. torch tensor data_ptr()) ----
+    def dist_begin(self, source):
+        d = C.c_int64()
+        _check(lib().bfsx_dist_begin(self._h, source, C.byref(d)))
+        return d.value
+
+    def dist_frontier_info(self):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().bfsx_dist_frontier_info(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def dist_td_expand(self, send_ptr, send_cap, nranks):
+        counts = np.zeros(nranks, np.int64)
+        _check(lib().bfsx_dist_td_expand(self._h, send_ptr, send_cap, _p(counts)))
+        return counts
+
+    def dist_td_claim(self, recv_ptr, n):
+        _check(lib().bfsx_dist_td_claim(self._h, recv_ptr, n))
+
+    def dist_frontier_slice(self, slice_ptr):
+        _check(lib().bfsx_dist_frontier_slice(self._h, slice_ptr))
+
+    def dist_bu_step(self, front_ptr):
+        _check(lib().bfsx_dist_bu_step(self._h, front_ptr))
+
+    def dist_level_end(self):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().bfsx_dist_level_end(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def dist_finish(self):
+        _check(lib().bfsx_dist_finish(self._h))
+
+    def dist_mcomp(self):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().bfsx_dist_mcomp(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def level_stats(self, cap=1 << 16):
         buf = (LevelStat * cap)()

@@ -239,15 +239,28 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
     return fail(BFSX_E_ARG, "unknown option " + k);
 }
 
-static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m,
-                                   bfsx_graph **out) {
+// rank/nranks > 1: 1-D partition -- this rank keeps the rows of global ids [rank*chunk, +chunk),
+// chunk = ceil(nv / nranks) rounded up to a multiple of 64 (frontier slices are whole bitmap words).
+static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m, int rank,
+                                   int nranks, bfsx_graph **out) {
     auto *g = new (std::nothrow) bfsx_graph();
     if (!g) return fail(BFSX_E_OOM, "graph");
     g->ctx = ctx;
-    g->nv = nv;
     g->m = m;
-    int rc = build_csr_device(ctx->stream, nv, d_u, d_v, m, ctx->opt.degree_order, &g->d_row_off, &g->d_col,
-                              &g->nnz, &g->d_tuple_cnt);
+    g->nv_global = nv;
+    g->rank = rank;
+    g->nranks = nranks;
+    if (nranks > 1) {
+        g->chunk = ((nv + nranks - 1) / nranks + 63) / 64 * 64;
+        g->v_lo = std::min<int64_t>((int64_t)rank * g->chunk, nv);
+        g->nv = std::min<int64_t>(g->chunk, nv - g->v_lo);
+    } else {
+        g->chunk = nv;
+        g->v_lo = 0;
+        g->nv = nv;
+    }
+    int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, &g->d_row_off, &g->d_col,
+                              &g->nnz, &g->d_tuple_cnt, g->v_lo, nv);
     if (rc) {
         delete g;
         return rc;
@@ -256,9 +269,10 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
     return BFSX_OK;
 }
 
-int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
-                          bfsx_graph **out) {
+static int graph_from_host_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
+                                 int rank, int nranks, bfsx_graph **out) {
     if (!ctx || !out || nv <= 0 || m < 0 || (m > 0 && (!u || !v))) return fail(BFSX_E_ARG, "bad argument");
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
     if (nv > (int64_t)INT32_MAX) return fail(BFSX_E_ARG, "nv must be < 2^31 on one device");
     for (int64_t i = 0; i < m; i++)
         if ((int64_t)u[i] >= nv || (int64_t)v[i] >= nv)
@@ -277,11 +291,21 @@ int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const ui
             hipMemcpyAsync(d_v, v, m * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
             rc = fail(BFSX_E_HIP, "H2D tuples");
     }
-    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, out);
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, rank, nranks, out);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(d_u);
     (void)hipFree(d_v);
     return rc;
+}
+
+int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
+                          bfsx_graph **out) {
+    return graph_from_host_edges(ctx, nv, u, v, m, 0, 1, out);
+}
+
+int bfsx_dist_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m, int rank,
+                               int nranks, bfsx_graph **out) {
+    return graph_from_host_edges(ctx, nv, u, v, m, rank, nranks, out);
 }
 
 int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
@@ -316,8 +340,10 @@ int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed
     return rc;
 }
 
-int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, bfsx_graph **out) {
+static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
+                           bfsx_graph **out) {
     if (!ctx || !out || scale < 1 || scale > 30 || edgefactor < 1) return fail(BFSX_E_ARG, "bad argument");
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
     BFSX_HIP_TRY(hipSetDevice(ctx->device));
     const int64_t nv = (int64_t)1 << scale;
     const int64_t m = (int64_t)edgefactor << scale;
@@ -328,10 +354,112 @@ int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed
         return fail(BFSX_E_OOM, "device tuples");
     }
     int rc = kronecker_generate(ctx->stream, scale, edgefactor, seed, d_u, d_v);
-    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, out);
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, rank, nranks, out);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(d_u);
     (void)hipFree(d_v);
+    return rc;
+}
+
+int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, bfsx_graph **out) {
+    return graph_kronecker(ctx, scale, edgefactor, seed, 0, 1, out);
+}
+
+int bfsx_dist_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
+                              bfsx_graph **out) {
+    return graph_kronecker(ctx, scale, edgefactor, seed, rank, nranks, out);
+}
+
+int bfsx_graph_partition(const bfsx_graph *g, int64_t *nv_global, int64_t *v_lo, int64_t *nv_local, int64_t *chunk,
+                         int32_t *rank, int32_t *nranks) {
+    if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (nv_global) *nv_global = g->nv_global;
+    if (v_lo) *v_lo = g->v_lo;
+    if (nv_local) *nv_local = g->nv;
+    if (chunk) *chunk = g->chunk;
+    if (rank) *rank = g->rank;
+    if (nranks) *nranks = g->nranks;
+    return BFSX_OK;
+}
+
+#define BFSX_DIST_GUARD(g)                                                                           \
+    do {                                                                                             \
+        if (!(g)) return fail(BFSX_E_ARG, "null graph");                                             \
+        BFSX_HIP_TRY(hipSetDevice((g)->ctx->device));                                                \
+    } while (0)
+
+int bfsx_graph_degree(const bfsx_graph *g, int64_t v, int64_t *deg) {
+    if (!g || !deg) return fail(BFSX_E_ARG, "bad argument");
+    *deg = -1;
+    if (v < g->v_lo || v >= g->v_lo + g->nv) return BFSX_OK;
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    int64_t off[2];
+    BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + (v - g->v_lo), sizeof(off), hipMemcpyDeviceToHost));
+    *deg = off[1] - off[0];
+    return BFSX_OK;
+}
+
+int bfsx_dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local) {
+    BFSX_DIST_GUARD(g);
+    int64_t d = 0;
+    int rc = dist_begin(g, source, &d);
+    if (deg_local) *deg_local = d;
+    return rc;
+}
+
+int bfsx_dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local) {
+    BFSX_DIST_GUARD(g);
+    int64_t a = 0, b = 0;
+    int q = 0;
+    int rc = dist_frontier_info(g, &a, &b, &q);
+    if (nf_local) *nf_local = a;
+    if (mf_local) *mf_local = b;
+    return rc;
+}
+
+int bfsx_dist_td_expand(bfsx_graph *g, void *d_send, int64_t send_cap, int64_t *send_counts) {
+    BFSX_DIST_GUARD(g);
+    if (!send_counts || (!d_send && send_cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    return dist_td_expand(g, (unsigned long long *)d_send, send_cap, send_counts);
+}
+
+int bfsx_dist_td_claim(bfsx_graph *g, const void *d_recv, int64_t n) {
+    BFSX_DIST_GUARD(g);
+    return dist_td_claim(g, (const unsigned long long *)d_recv, n);
+}
+
+int bfsx_dist_frontier_slice(bfsx_graph *g, void *d_slice) {
+    BFSX_DIST_GUARD(g);
+    if (!d_slice) return fail(BFSX_E_ARG, "null slice");
+    return dist_frontier_slice(g, (unsigned long long *)d_slice);
+}
+
+int bfsx_dist_bu_step(bfsx_graph *g, const void *d_front_global) {
+    BFSX_DIST_GUARD(g);
+    if (!d_front_global) return fail(BFSX_E_ARG, "null frontier");
+    return dist_bu_step(g, (const unsigned long long *)d_front_global);
+}
+
+int bfsx_dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local) {
+    BFSX_DIST_GUARD(g);
+    int64_t a = 0, b = 0;
+    int rc = dist_level_end(g, &a, &b);
+    if (nf_local) *nf_local = a;
+    if (mf_local) *mf_local = b;
+    return rc;
+}
+
+int bfsx_dist_finish(bfsx_graph *g) {
+    BFSX_DIST_GUARD(g);
+    return dist_finish(g);
+}
+
+int bfsx_dist_mcomp(bfsx_graph *g, int64_t *m_local, int64_t *reached_local) {
+    BFSX_DIST_GUARD(g);
+    int64_t a = 0, b = 0;
+    int rc = bfs_mcomp(g, &a, &b);
+    if (m_local) *m_local = a;
+    if (reached_local) *reached_local = b;
     return rc;
 }
 
@@ -364,6 +492,7 @@ int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col) {
 
 int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
     if (!g || !roots || count < 0) return fail(BFSX_E_ARG, "bad argument");
+    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: sample roots with bfsx_graph_degree");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     std::unordered_set<int64_t> seen;
     int found = 0;
@@ -389,6 +518,7 @@ int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
 
 int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: drive it with bfsx_dist_* (bfsx_dist.py)");
     const auto t0 = std::chrono::steady_clock::now();
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     bfsx_stats local{};

@@ -123,16 +123,19 @@ __device__ inline void shard_add(LevelSlot *slot, unsigned long long nf, unsigne
 }
 
 // ---- K2: source init (after the visited bitmap is reset to the dead mask) -------------------------
-__global__ void k_init_source(uint32_t s, int64_t prev, const unsigned long long *__restrict__ dead,
+// s: local row of the source (0xFFFFFFFF: the source is owned by another rank); sglob: its global id.
+__global__ void k_init_source(uint32_t s, uint32_t sglob, int64_t prev, const unsigned long long *__restrict__ dead,
                               int32_t *dist, int32_t *parent, unsigned long long *vis, uint32_t *q,
                               LevelSlot *ring) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         // a previous isolated source is pre-visited (dead mask) so k_finalize never resets it
         if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) dist[prev] = INT32_MAX;
-        dist[s] = 0;
-        parent[s] = (int32_t)s;
-        vis[s >> 6] |= 1ull << (s & 63u);
-        q[0] = s;
+        if (s != 0xFFFFFFFFu) {
+            dist[s] = 0;
+            parent[s] = (int32_t)sglob;
+            vis[s >> 6] |= 1ull << (s & 63u);
+            q[0] = s;
+        }
     }
     zero_slot(ring, -2); // slot 0
     zero_slot(ring, -1); // slot 1
@@ -835,7 +838,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, nwords * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, (uint32_t)source, ws->prev_source, ws->dead,
+    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, (uint32_t)source, (uint32_t)source, ws->prev_source, ws->dead,
                        ws->dist, ws->parent, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
     ws->prev_source = source;
@@ -1000,6 +1003,257 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         for (size_t i = 0; i < nv; i++) parent_out[i] = (dist[i] == INT32_MAX) ? -1 : (int64_t)p32[i];
     } else {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
+    }
+    return BFSX_OK;
+}
+
+// ==== multi-GPU level primitives (1-D partition) ====================================================
+// The level loop of a partitioned BFS runs in the caller (bfsx_dist.py over torch.distributed: RCCL
+// on device buffers), which owns the exchange buffers and passes their device pointers in:
+//   begin -> per level { td_expand -> all-to-all(pairs) -> td_claim | frontier_slice -> all-gather ->
+//   bu_step } -> level_end (local counts; the caller all-reduces) -> finish.
+namespace {
+
+inline Part make_part(bfsx_graph *g, BfsWorkspace *ws) {
+    Part p{};
+    p.lo = (uint32_t)g->v_lo;
+    p.chunk = (uint32_t)g->chunk;
+    p.rank = (uint32_t)g->rank;
+    p.remote = ws->remote;
+    p.remote_tail = ws->d_dist_ctr;
+    return p;
+}
+
+int dist_ws(bfsx_graph *g) {
+    int rc = ws_alloc(g);
+    if (rc) return rc;
+    if (!g->ws->d_dist_ctr)
+        BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, (1 + 2 * kMaxRanks) * sizeof(unsigned long long)));
+    return BFSX_OK;
+}
+
+int dist_level_events(BfsWorkspace *ws, int level) {
+    while ((int)ws->ev_level.size() <= level) {
+        hipEvent_t e0, e1;
+        BFSX_HIP_TRY(hipEventCreate(&e0));
+        BFSX_HIP_TRY(hipEventCreate(&e1));
+        ws->ev_begin.push_back(e0);
+        ws->ev_level.push_back(e1);
+    }
+    return BFSX_OK;
+}
+
+} // namespace
+
+int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local) {
+    if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
+    int rc = dist_ws(g);
+    if (rc) return rc;
+    BfsWorkspace *ws = g->ws;
+    hipStream_t st = g->ctx->stream;
+    const bool owned = source >= g->v_lo && source < g->v_lo + g->nv;
+    const int64_t sl = owned ? source - g->v_lo : -1;
+    int64_t deg = 0;
+    if (owned) {
+        int64_t so[2];
+        BFSX_HIP_TRY(hipMemcpy(so, g->d_row_off + sl, sizeof(so), hipMemcpyDeviceToHost));
+        deg = so[1] - so[0];
+    }
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, ws->nwords * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)source,
+                       ws->prev_source, ws->dead, ws->dist, ws->parent, ws->vis, ws->qa, ws->ring);
+    BFSX_HIP_TRY(hipGetLastError());
+    ws->prev_source = sl;
+    ws->d_level = 0;
+    ws->d_dir = BFSX_DIR_TOPDOWN;
+    ws->d_in_queue = true;
+    ws->d_nf = owned ? 1 : 0;
+    ws->d_mf = deg;
+    g->level_dirs.clear();
+    g->level_cum_ms.clear();
+    g->level_stats.clear();
+    g->last_source = source;
+    *deg_local = deg;
+    return BFSX_OK;
+}
+
+int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue) {
+    if (!g->ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    *nf_local = g->ws->d_nf;
+    *mf_local = g->ws->d_mf;
+    *in_queue = g->ws->d_in_queue ? 1 : 0;
+    return BFSX_OK;
+}
+
+int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, int64_t *send_counts) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    hipStream_t st = g->ctx->stream;
+    const Options &opt = g->ctx->opt;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    const int level = ws->d_level, P = g->nranks;
+    if (int rc2 = dist_level_events(ws, level)) return rc2;
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
+    if (!ws->d_in_queue) { // frontier held as a local bitmap slice (after a bottom-up level)
+        BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(unsigned long long), st));
+        const int64_t per_block_min = (int64_t)kBS * kCompactWords;
+        const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
+        const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
+        hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
+                           ws->d_cursor);
+        BFSX_HIP_TRY(hipGetLastError());
+        ws->d_in_queue = true;
+    }
+    // remote pairs <= adjacency entries of the local frontier
+    const int64_t need = std::max<int64_t>(ws->d_mf, 1);
+    if (need > ws->remote_cap) {
+        if (ws->remote) BFSX_HIP_TRY(hipFree(ws->remote));
+        ws->remote = nullptr;
+        ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
+        BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(unsigned long long)));
+    }
+    if (send_cap < ws->d_mf) return fail(BFSX_E_ARG, "send buffer smaller than the local frontier's m_f");
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, (1 + 2 * kMaxRanks) * sizeof(unsigned long long), st));
+    const Part pt = make_part(g, ws);
+    hipLaunchKernelGGL(k_td<true>, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, g->d_row_off,
+                       g->d_col, ws->qa, (uint32_t)ws->d_nf, ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level,
+                       opt.hub_degree, ws->hubs, pt);
+    BFSX_HIP_TRY(hipGetLastError());
+    if (ws->d_mf > (int64_t)opt.hub_degree) {
+        const dim3 gh(clamp_grid((ws->d_mf + kBS * kItems - 1) / (kBS * kItems), cap));
+        hipLaunchKernelGGL(k_td_hubs<true>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs, ws->qb, ws->vis,
+                           ws->dist, ws->parent, ws->ring, level, pt);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    unsigned long long n_remote = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&n_remote, ws->d_dist_ctr, sizeof(n_remote), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    unsigned long long *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
+    if (n_remote > 0) {
+        const unsigned gbk = clamp_grid(((int64_t)n_remote + kBS - 1) / kBS, 1024);
+        hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, (uint64_t)n_remote,
+                           (uint32_t)g->chunk, P, dcount);
+        BFSX_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, (uint64_t)n_remote,
+                           (uint32_t)g->chunk, P, dcount, dcursor, d_send);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    std::vector<unsigned long long> h(P, 0);
+    BFSX_HIP_TRY(hipMemcpyAsync(h.data(), dcount, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    for (int p = 0; p < P; p++) send_counts[p] = (int64_t)h[p];
+    ws->d_dir = BFSX_DIR_TOPDOWN;
+    return BFSX_OK;
+}
+
+int dist_td_claim(bfsx_graph *g, const unsigned long long *d_recv, int64_t n) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    if (n <= 0) return BFSX_OK;
+    hipStream_t st = g->ctx->stream;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    hipLaunchKernelGGL(k_claim_remote, dim3(clamp_grid((n + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, d_recv,
+                       (uint32_t)n, g->d_row_off, ws->vis, ws->dist, ws->parent, ws->qb, ws->ring, ws->d_level,
+                       (uint32_t)g->v_lo);
+    BFSX_HIP_TRY(hipGetLastError());
+    return BFSX_OK;
+}
+
+int dist_frontier_slice(bfsx_graph *g, unsigned long long *d_slice) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    hipStream_t st = g->ctx->stream;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    if (int rc2 = dist_level_events(ws, ws->d_level)) return rc2;
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[ws->d_level], st));
+    if (ws->d_in_queue) {
+        BFSX_HIP_TRY(hipMemsetAsync(d_slice, 0, ws->nwords * sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
+                           ws->qa, (uint32_t)ws->d_nf, d_slice);
+        BFSX_HIP_TRY(hipGetLastError());
+    } else {
+        BFSX_HIP_TRY(hipMemcpyAsync(d_slice, ws->front, ws->nwords * sizeof(unsigned long long),
+                                    hipMemcpyDeviceToDevice, st));
+    }
+    BFSX_HIP_TRY(hipStreamSynchronize(st)); // the caller hands the slice to a collective next
+    return BFSX_OK;
+}
+
+int dist_bu_step(bfsx_graph *g, const unsigned long long *d_front_global) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    hipStream_t st = g->ctx->stream;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    hipLaunchKernelGGL(k_bu, dim3(clamp_grid((ws->nwords + kWaves * 64 - 1) / (kWaves * 64), cap)), dim3(kBS), 0, st,
+                       g->d_row_off, g->d_col, ws->top1, d_front_global, ws->next, ws->vis, ws->dist, ws->parent,
+                       ws->ring, ws->d_level, ws->nwords);
+    BFSX_HIP_TRY(hipGetLastError());
+    ws->d_dir = BFSX_DIR_BOTTOMUP;
+    ws->d_in_queue = false;
+    return BFSX_OK;
+}
+
+int dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    hipStream_t st = g->ctx->stream;
+    const int level = ws->d_level;
+    if (int rc2 = dist_level_events(ws, level)) return rc2;
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->h_slot, ws->ring + (level + 1) % 3, sizeof(LevelSlot), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    int64_t s_nf = 0, s_mf = 0, s_sc = 0, s_cl = 0;
+    for (int i = 0; i < kShards; i++) {
+        s_nf += (int64_t)ws->h_slot->sh[i].nf;
+        s_mf += (int64_t)ws->h_slot->sh[i].mf;
+        s_sc += (int64_t)ws->h_slot->sh[i].scanned;
+        s_cl += (int64_t)ws->h_slot->sh[i].claims;
+    }
+    const bool td = ws->d_dir == BFSX_DIR_TOPDOWN;
+    const int64_t nf_new = td ? (int64_t)ws->h_slot->qtail : s_nf;
+    bfsx_level_stat ls{};
+    ls.direction = ws->d_dir;
+    ls.level = level;
+    ls.frontier_in = ws->d_nf;
+    ls.frontier_out = nf_new;
+    ls.mf_in = ws->d_mf;
+    ls.scanned = td ? ws->d_mf : s_sc;
+    ls.claims = s_cl;
+    g->level_stats.push_back(ls);
+    g->level_dirs.push_back(ws->d_dir);
+    if (td) std::swap(ws->qa, ws->qb);
+    else std::swap(ws->front, ws->next);
+    ws->d_in_queue = td;
+    ws->d_nf = nf_new;
+    ws->d_mf = s_mf;
+    ws->d_level = level + 1;
+    *nf_local = nf_new;
+    *mf_local = s_mf;
+    return BFSX_OK;
+}
+
+int dist_finish(bfsx_graph *g) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
+    hipStream_t st = g->ctx->stream;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis,
+                       ws->nwords, ws->dist);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
+    BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
+    const int levels = ws->d_level;
+    g->level_cum_ms.resize(levels);
+    for (int l = 0; l < levels; l++) {
+        float t = 0.f, k = 0.f;
+        BFSX_HIP_TRY(hipEventElapsedTime(&t, ws->ev_start, ws->ev_level[l]));
+        BFSX_HIP_TRY(hipEventElapsedTime(&k, ws->ev_begin[l], ws->ev_level[l]));
+        g->level_cum_ms[l] = t;
+        if (l < (int)g->level_stats.size()) {
+            g->level_stats[l].cum_ms = t;
+            g->level_stats[l].kernel_ms = k;
+        }
     }
     return BFSX_OK;
 }

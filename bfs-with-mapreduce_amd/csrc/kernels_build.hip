@@ -34,24 +34,39 @@ inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap = 16384) 
     return (unsigned)g;
 }
 
+// Rows are built only for global ids in [lo, lo + nv) (the whole graph on one device); indices into
+// deg / tcnt / cursor are local (id - lo), adjacency entries stay global.
 __global__ __launch_bounds__(kBS) void k_count(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
-                                               int64_t m, uint32_t *__restrict__ deg,
+                                               int64_t m, uint32_t lo, uint32_t nv, uint32_t *__restrict__ deg,
                                                uint32_t *__restrict__ tcnt) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
-        uint32_t a = u[i], b = v[i];
-        atomicAdd(&deg[a], 1u);
-        if (a != b) atomicAdd(&deg[b], 1u);
-        atomicAdd(&tcnt[a], 1u);
+        const uint32_t a = u[i] - lo, b = v[i] - lo; // unsigned wrap: out of range -> >= nv
+        if (a < nv) {
+            atomicAdd(&deg[a], 1u);
+            atomicAdd(&tcnt[a], 1u);
+        }
+        if (b < nv && a != b) atomicAdd(&deg[b], 1u);
     }
 }
 
 __global__ __launch_bounds__(kBS) void k_scatter(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
-                                                 int64_t m, unsigned long long *__restrict__ cursor,
-                                                 uint32_t *__restrict__ col) {
+                                                 int64_t m, uint32_t lo, uint32_t nv,
+                                                 unsigned long long *__restrict__ cursor, uint32_t *__restrict__ col) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
-        uint32_t a = u[i], b = v[i];
-        col[atomicAdd(&cursor[a], 1ull)] = b;
-        if (a != b) col[atomicAdd(&cursor[b], 1ull)] = a;
+        const uint32_t a = u[i], b = v[i];
+        if (a - lo < nv) col[atomicAdd(&cursor[a - lo], 1ull)] = b;
+        if (b - lo < nv && a != b) col[atomicAdd(&cursor[b - lo], 1ull)] = a;
+    }
+}
+
+// Degree of every global id over the whole tuple list (duplicates counted): the row-order key of a
+// partitioned graph, whose neighbours' rows live on other ranks.
+__global__ __launch_bounds__(kBS) void k_count_all(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
+                                                   int64_t m, uint32_t *__restrict__ deg) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
+        const uint32_t a = u[i], b = v[i];
+        atomicAdd(&deg[a], 1u);
+        if (a != b) atomicAdd(&deg[b], 1u);
     }
 }
 
@@ -228,11 +243,13 @@ int sort_rows(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz,
 }
 
 // Key for the degree-descending row order: (UINT32_MAX - deg(nbr)) << 32 | nbr.
+// gdeg (partitioned graphs): global degree table; otherwise the degree comes from the local CSR.
 __global__ __launch_bounds__(kBS) void k_degree_keys(const int64_t *__restrict__ off, const uint32_t *__restrict__ col,
-                                                     int64_t nnz, unsigned long long *__restrict__ keys) {
+                                                     const uint32_t *__restrict__ gdeg, int64_t nnz,
+                                                     unsigned long long *__restrict__ keys) {
     for (int64_t j = (int64_t)blockIdx.x * kBS + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * kBS) {
         const uint32_t x = col[j];
-        const uint64_t d = (uint64_t)(off[x + 1] - off[x]);
+        const uint64_t d = gdeg ? (uint64_t)gdeg[x] : (uint64_t)(off[x + 1] - off[x]);
         const uint64_t dk = d >= 0xFFFFFFFFull ? 0ull : 0xFFFFFFFFull - d;
         keys[j] = (dk << 32) | x;
     }
@@ -246,12 +263,14 @@ __global__ __launch_bounds__(kBS) void k_low32(const unsigned long long *__restr
 
 // Re-order every row so that high-degree neighbours come first: a bottom-up probe of an unvisited
 // vertex then tests the neighbour most likely to be in a large frontier first (early exit).
-int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz, uint32_t *d_col) {
+int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz, uint32_t *d_col,
+                         const uint32_t *gdeg) {
     if (nnz <= 0) return BFSX_OK;
     DevBuf<unsigned long long> k0, k1;
     BFSX_HIP_TRY(k0.alloc(nnz));
     BFSX_HIP_TRY(k1.alloc(nnz));
-    hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(nnz, kBS)), dim3(kBS), 0, stream, d_off, d_col, nnz, k0.p);
+    hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(nnz, kBS)), dim3(kBS), 0, stream, d_off, d_col, gdeg, nnz,
+                       k0.p);
     BFSX_HIP_TRY(hipGetLastError());
     int rc = sort_rows(stream, d_off, nv, nnz, k0.p, k1.p, 64u);
     if (rc) return rc;
@@ -263,7 +282,9 @@ int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, i
 
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
                      bool degree_order, int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out,
-                     uint32_t **d_tuple_cnt_out) {
+                     uint32_t **d_tuple_cnt_out, int64_t lo, int64_t nv_global) {
+    if (nv_global < 0) nv_global = nv;
+    const bool partitioned = lo != 0 || nv != nv_global;
     DevBuf<uint32_t> deg, tcnt;
     DevBuf<int64_t> off;
     BFSX_HIP_TRY(deg.alloc(nv + 1));
@@ -272,7 +293,8 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
     BFSX_HIP_TRY(hipMemsetAsync(deg.p, 0, (nv + 1) * sizeof(uint32_t), stream));
     BFSX_HIP_TRY(hipMemsetAsync(tcnt.p, 0, nv * sizeof(uint32_t), stream));
     if (m > 0) {
-        hipLaunchKernelGGL(k_count, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, deg.p, tcnt.p);
+        hipLaunchKernelGGL(k_count, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, (uint32_t)lo,
+                           (uint32_t)nv, deg.p, tcnt.p);
         BFSX_HIP_TRY(hipGetLastError());
     }
     // K1b: row offsets (int64) = exclusive scan of degrees
@@ -298,8 +320,8 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
         BFSX_HIP_TRY(cursor.alloc(nv));
         BFSX_HIP_TRY(hipMemcpyAsync(cursor.p, off.p, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
         if (m > 0) {
-            hipLaunchKernelGGL(k_scatter, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m,
-                               (unsigned long long *)cursor.p, col.p);
+            hipLaunchKernelGGL(k_scatter, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, (uint32_t)lo,
+                               (uint32_t)nv, (unsigned long long *)cursor.p, col.p);
             BFSX_HIP_TRY(hipGetLastError());
         }
         BFSX_HIP_TRY(hipStreamSynchronize(stream));
@@ -310,7 +332,7 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
     BFSX_HIP_TRY(col_s.alloc(nnz_raw));
     {
         unsigned end_bit = 1;
-        while (end_bit < 32 && (1ULL << end_bit) < (uint64_t)nv) end_bit++;
+        while (end_bit < 32 && (1ULL << end_bit) < (uint64_t)nv_global) end_bit++;
         int rc = sort_rows(stream, off.p, nv, nnz_raw, col.p, col_s.p, end_bit);
         if (rc) return rc;
     }
@@ -358,7 +380,16 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
     keep.reset();
     pos.reset();
     if (degree_order) {
-        int rc = order_rows_by_degree(stream, noff.p, nv, nnz, col_f.p);
+        DevBuf<uint32_t> gdeg;
+        if (partitioned) {
+            BFSX_HIP_TRY(gdeg.alloc(nv_global));
+            BFSX_HIP_TRY(hipMemsetAsync(gdeg.p, 0, nv_global * sizeof(uint32_t), stream));
+            if (m > 0) {
+                hipLaunchKernelGGL(k_count_all, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, gdeg.p);
+                BFSX_HIP_TRY(hipGetLastError());
+            }
+        }
+        int rc = order_rows_by_degree(stream, noff.p, nv, nnz, col_f.p, gdeg.p);
         if (rc) return rc;
     }
 
