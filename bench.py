@@ -1,10 +1,14 @@
 """Benchmark: GTEPS (harmonic mean over roots) on Graph500 Kronecker scale-26, edgefactor 16.
 
 A "step" is one BFS from one root over the device-resident CSR (BASELINE.json configs[3]); the graph
-is generated and built on the GPU before the timed region.  Per root, t_bfs = device time from
-source init to the last level (hipEvents inside libbfsx.so); TEPS = m_comp / t_bfs with m_comp = the
-input tuples inside the root's component (Graph500 convention).  value = harmonic mean GTEPS over the
-K timed roots (= K*m / sum t when every root lies in the giant component).
+is generated and built on the GPU before the timed region.  TEPS per root = m_comp / t with m_comp =
+the input tuples inside the root's component (Graph500 convention); value = harmonic mean GTEPS over
+the K timed roots (= K*m / sum t when every root lies in the giant component).
+
+  N = 1: t = device time from source init to the last level (hipEvents inside libbfsx.so).
+  N > 1: launched as one process per GPU (torch.distributed.run); the graph is 1-D partitioned over
+         the ranks (bfsx_dist.py) and every level exchanges over RCCL (backend "nccl"); t = the max
+         over ranks of the wall time of one BFS, bracketed by barrier + device synchronise.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
 
@@ -13,7 +17,6 @@ Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline acc
 import argparse
 import importlib.util
 import json
-import math
 import os
 import sys
 import time
@@ -21,28 +24,33 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "bfs-with-mapreduce_amd")
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def load_bfsx():
-    spec = importlib.util.spec_from_file_location("bfsx", os.path.join(ROOT, "bfs-with-mapreduce_amd", "bfsx.py"))
+def load_module(name, file):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, file))
     mod = importlib.util.module_from_spec(spec)
-    sys.modules["bfsx"] = mod
+    sys.modules[name] = mod
     spec.loader.exec_module(mod)
     return mod
 
 
 def level_bytes(ls, nwords):
-    """Algorithmic bytes of one level (DESIGN.md "Roofline accounting")."""
-    if ls["direction"] == 2:  # bottom-up: visited word read + next word write, row offsets of the
-        # unvisited candidates, adjacency entries actually scanned, dist+parent of the found
-        return 16 * nwords + 8 * ls["unvisited_in"] + 4 * ls["scanned"] + 8 * ls["frontier_out"]
+    """Algorithmic bytes of one level."""
+    if ls["direction"] == 2:  # bottom-up: visited word read + next word write, row offsets and top1
+        # of the live unvisited candidates, adjacency entries scanned, dist+parent of the found
+        return 16 * nwords + 12 * max(ls["unvisited_in"], 0) + 4 * ls["scanned"] + 8 * ls["frontier_out"]
     # top-down: queue read, row offsets (2 x 8 B per frontier vertex), adjacency rows, winners'
     # dist+parent writes, queue append, degree lookups of the winners
-    return 4 * ls["frontier_in"] + 16 * ls["frontier_in"] + 4 * max(ls["mf_in"], 0) + 28 * ls["frontier_out"]
+    return 20 * ls["frontier_in"] + 4 * max(ls["mf_in"], 0) + 28 * ls["frontier_out"]
 
 
-def main():
+def hmean(xs):
+    return len(xs) / sum(1.0 / x for x in xs)
+
+
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=64)
@@ -56,24 +64,58 @@ def main():
     ap.add_argument("--direction", default="auto")
     ap.add_argument("--levels-json", default="")
     ap.add_argument("--option", action="append", default=[], help="libbfsx option key=value")
-    args = ap.parse_args()
+    ap.add_argument("--dist", action="store_true", help="use the partitioned path even on one rank (rehearsal)")
+    return ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    bfsx = load_bfsx()
-    dist_mod = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist_mod
 
-        dist_mod.init_process_group("gloo")
+def common_fields(args, world, value, wall, nv, m, nnz, nroots, parallelism):
+    return {
+        "metric": f"GTEPS (harmonic mean, {args.steps} roots) on RMAT scale-{args.scale}",
+        "value": value,
+        "unit": "GTEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall * 1e3 / max(args.steps, 1),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (Graph500 Kronecker A/B/C/D=.57/.19/.19/.05, generated on device)",
+        "config": {
+            "workload": f"kronecker-s{args.scale}-ef{args.edgefactor}",
+            "scale": args.scale,
+            "edgefactor": args.edgefactor,
+            "seed": hex(args.seed),
+            "nv": nv,
+            "m_tuples": m,
+            "nnz_directed": nnz,
+            "roots": nroots,
+            "direction": args.direction,
+            "parallelism": parallelism,
+        },
+    }
 
-    def barrier():
-        if dist_mod is not None:
-            dist_mod.barrier()
 
-    ctx = bfsx.Context(local_rank, direction=args.direction)
+def roofline(bu_bytes, bu_ms, bu_launches, note):
+    ach = (bu_bytes / bu_launches) / ((bu_ms / bu_launches) * 1e-3) / 1e9 if bu_launches else 0.0
+    return {
+        "bound": "hbm",
+        "kernel": "k_bu (bottom-up pull)",
+        "achieved": round(ach, 1),
+        "peak": PEAK_HBM_GBS,
+        "unit": "GB/s",
+        "frac": round(ach / PEAK_HBM_GBS, 4),
+        "traffic": None,
+        "launches": bu_launches,
+        "avg_launch_ms": round(bu_ms / max(bu_launches, 1), 4),
+        "note": note,
+    }
+
+
+def run_single(args):
+    bfsx = load_module("bfsx", "bfsx.py")
+    ctx = bfsx.Context(0, direction=args.direction)
     for kv in args.option:
         k, val = kv.split("=", 1)
         ctx.set_option(k, val)
@@ -81,8 +123,7 @@ def main():
     g = ctx.kronecker(args.scale, args.edgefactor, args.seed)
     build_s = time.perf_counter() - t0
     nv, nwords = g.nv, (g.nv + 63) // 64
-    n_roots = max(args.steps, 1)
-    roots = g.sample_roots(min(n_roots, 64), seed=args.root_seed + rank)
+    roots = g.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)
     # untimed pass: m_comp per root (Graph500 counts input tuples inside the root's component)
     mcomp = {}
     for r in roots:
@@ -93,9 +134,8 @@ def main():
         g.bfs_device_only(r)
 
     ctx.synchronize()
-    barrier()
     w0 = time.perf_counter()
-    t_bfs, bu_bytes, bu_ms, bu_launches, td_ms, all_levels = [], 0, 0.0, 0, 0.0, []
+    t_bfs, bu_bytes, bu_ms, bu_launches, all_levels = [], 0, 0.0, 0, []
     for r in order[args.warmup:]:
         t_bfs.append(g.bfs_device_only(r))
         for ls in g.level_stats(256):
@@ -103,119 +143,141 @@ def main():
                 bu_bytes += level_bytes(ls, nwords)
                 bu_ms += ls["kernel_ms"]
                 bu_launches += 1
-            else:
-                td_ms += ls["kernel_ms"]
             if args.levels_json:
                 all_levels.append(dict(ls, root=r))
     ctx.synchronize()
-    barrier()
     wall = time.perf_counter() - w0
-    if dist_mod is not None:
-        import torch
-
-        tw = torch.tensor([wall], dtype=torch.float64)
-        dist_mod.all_reduce(tw, op=dist_mod.ReduceOp.MAX)
-        wall = float(tw[0])
 
     steps_roots = order[args.warmup:]
     gteps = [mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(steps_roots, t_bfs)]
-    hmean = len(gteps) / sum(1.0 / x for x in gteps)
-    total = hmean
-    if dist_mod is not None:  # independent replicas: aggregate = sum of per-rank rates
-        th = torch.tensor([hmean], dtype=torch.float64)
-        dist_mod.all_reduce(th, op=dist_mod.ReduceOp.SUM)
-        total = float(th[0])
-    m_mean = float(np.mean([mcomp[r] for r in steps_roots]))
-    # survey 8(d) edge-scan model: B = 4*(2M) + 12*n per BFS
-    bfs_bytes = 8.0 * g.m + 12.0 * nv
+    bfs_bytes = 8.0 * g.m + 12.0 * nv  # SURVEY 8(d) edge-scan model: B = 4*(2M) + 12*n per BFS
     bfs_ach = bfs_bytes / (np.mean(t_bfs) * 1e-3) / 1e9
-    bu_ach = (bu_bytes / bu_launches) / ((bu_ms / bu_launches) * 1e-3) / 1e9 if bu_launches else 0.0
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
+    if not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_py as O  # cpu_baseline leg only
 
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         off, col = g.csr()
-        samples = []
-        spent = 0.0
+        samples, spent = [], 0.0
         for r in roots:
             c0 = time.perf_counter()
             res = O.mapreduce_bfs(nv, off, col, int(r), nthreads=nthreads, max_iters=1)
             dt = time.perf_counter() - c0
-            d_gpu, _ = g.bfs(int(r), want_parent=False)[:2]
+            d_gpu = g.bfs(int(r), want_parent=False)[0]
             assert np.array_equal(res["dist"], d_gpu), "CPU oracle and GPU disagree"
             samples.append(mcomp[int(r)] / dt / 1e9)
             spent += dt
             if spent >= args.cpu_baseline_seconds:
                 break
         cpu = {
-            "value": len(samples) / sum(1.0 / x for x in samples),
+            "value": hmean(samples),
             "unit": "GTEPS",
             "cores": nthreads,
             "kind": "port",
-            "sample": f"{len(samples)} root(s) of the same scale-{args.scale} graph, oracle "
-                      f"orc_mapreduce_bfs (BfsSpark map/reduce restated, OpenMP), {spent:.1f} s",
+            "sample": f"{len(samples)} root(s) of the same scale-{args.scale} graph, oracle orc_mapreduce_bfs "
+                      f"(BfsSpark map/reduce restated, OpenMP), {spent:.1f} s; distances asserted equal to the GPU's",
         }
         del off, col
 
-    out = {
-        "metric": f"GTEPS (harmonic mean, {len(t_bfs)} roots) on RMAT scale-{args.scale}",
-        "value": total,
-        "unit": "GTEPS",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": wall * 1e3 / max(args.steps, 1),
-        "higher_is_better": True,
-        "scaling": "weak" if world > 1 else "strong",
-        "vs_baseline": None,
-        "dtype": "int32",
-        "data": "synthetic (Graph500 Kronecker A/B/C/D=.57/.19/.19/.05, generated on device)",
-        "config": {
-            "workload": f"kronecker-s{args.scale}-ef{args.edgefactor}",
-            "scale": args.scale,
-            "edgefactor": args.edgefactor,
-            "seed": hex(args.seed),
-            "nv": nv,
-            "m_tuples": g.m,
-            "nnz_directed": g.nnz,
-            "roots": len(roots),
-            "direction": args.direction,
-            "parallelism": "replica" if world > 1 else "single",
-        },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "k_bu (bottom-up pull)",
-            "achieved": round(bu_ach, 1),
-            "peak": PEAK_HBM_GBS,
-            "unit": "GB/s",
-            "frac": round(bu_ach / PEAK_HBM_GBS, 4),
-            "traffic": None,
-            "launches": bu_launches,
-            "avg_launch_ms": round(bu_ms / max(bu_launches, 1), 4),
-        },
-        "bfs_roofline": {
-            "model": "B = 4*(2M) + 12*n per BFS (SURVEY 8d)",
-            "achieved_GBs": round(bfs_ach, 1),
-            "frac": round(bfs_ach / PEAK_HBM_GBS, 4),
-        },
-        "t_bfs_ms_mean": float(np.mean(t_bfs)),
-        "t_bfs_ms_min": float(np.min(t_bfs)),
-        "m_comp_mean": m_mean,
-        "graph_build_s": round(build_s, 3),
-        "cpu_baseline": cpu,
-    }
-    if args.levels_json and rank == 0:
+    out = common_fields(args, 1, hmean(gteps), wall, nv, g.m, g.nnz, len(roots), "single")
+    out["roofline"] = roofline(bu_bytes, bu_ms, bu_launches,
+                               "algorithmic bytes of every bottom-up level / its hipEvent duration")
+    out["bfs_roofline"] = {"model": "B = 4*(2M) + 12*n per BFS (SURVEY 8d)",
+                           "achieved_GBs": round(bfs_ach, 1), "frac": round(bfs_ach / PEAK_HBM_GBS, 4)}
+    out.update({"t_bfs_ms_mean": float(np.mean(t_bfs)), "t_bfs_ms_min": float(np.min(t_bfs)),
+                "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])), "graph_build_s": round(build_s, 3),
+                "cpu_baseline": cpu})
+    if args.levels_json:
         with open(args.levels_json, "w") as f:
             json.dump(all_levels, f)
+    print(json.dumps(out), flush=True)
+    g.free()
+    ctx.close()
+
+
+def run_dist(args, world, rank, local_rank):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dist.init_process_group("nccl")  # RCCL over xGMI
+    bfsx = load_module("bfsx", "bfsx.py")
+    bd = load_module("bfsx_dist", "bfsx_dist.py")
+    opts = dict(kv.split("=", 1) for kv in args.option)
+    ctx = bfsx.Context(local_rank, direction=args.direction)
+    for k, val in opts.items():
+        if k not in ("alpha", "beta"):
+            ctx.set_option(k, val)
+    dev = torch.device("cuda", local_rank)
+    t0 = time.perf_counter()
+    g = ctx.dist_kronecker(args.scale, rank, world, args.edgefactor, args.seed)
+    build_s = time.perf_counter() - t0
+    eng = bd.GpuEngine(torch, g, dev)
+    comm = bd.Comm(torch, dist, dev, staging=False)
+    drv = bd.DistBFS(eng, comm, direction=args.direction, alpha=int(opts.get("alpha", 30)),
+                     beta=int(opts.get("beta", 24)))
+    roots = drv.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)
+    mcomp = {}
+    for r in roots:
+        drv.run(r)
+        mcomp[r] = drv.mcomp()[0]
+    order = [roots[i % len(roots)] for i in range(args.warmup + args.steps)]
+    for r in order[: args.warmup]:
+        drv.run(r)
+
+    def timed(r):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        a = time.perf_counter()
+        drv.run(r)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - a
+
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    w0 = time.perf_counter()
+    local_t = [timed(r) for r in order[args.warmup:]]
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    wall = time.perf_counter() - w0
+    tt = torch.tensor(local_t + [wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)  # max over ranks, per root
+    t_root = tt[:-1].cpu().tolist()
+    wall = float(tt[-1])
+    steps_roots = order[args.warmup:]
+    gteps = [mcomp[r] / t / 1e9 for r, t in zip(steps_roots, t_root)]
+    nnz = comm.allreduce_i64([g.nnz])[0]
     if rank == 0:
+        out = common_fields(args, world, hmean(gteps), wall, eng.nv_global, g.m, nnz, len(roots),
+                            f"1d-partition dp{world} (RCCL all-to-all + all-gather)")
+        bu_bytes, bu_ms, bu_launches = 0, 0.0, 0
+        for ls in g.level_stats(256):  # rank 0's last BFS: kernel time incl. the all-gather wait
+            if ls["direction"] == 2:
+                bu_bytes += level_bytes(dict(ls, unvisited_in=eng.nv_local), eng.slice_words)
+                bu_ms += ls["kernel_ms"]
+                bu_launches += 1
+        out["roofline"] = roofline(bu_bytes, bu_ms, bu_launches,
+                                   "rank 0, last BFS; bottom-up level time includes the all-gather wait; "
+                                   "unvisited_in bounded by the local row count")
+        out.update({"t_bfs_ms_mean": float(np.mean(t_root)) * 1e3, "t_bfs_ms_min": float(np.min(t_root)) * 1e3,
+                    "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])),
+                    "graph_build_s": round(build_s, 3), "cpu_baseline": None,
+                    "levels_last": drv.level_log})
         print(json.dumps(out), flush=True)
     g.free()
     ctx.close()
-    if dist_mod is not None:
-        dist_mod.destroy_process_group()
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.dist:
+        run_dist(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
+    else:
+        run_single(args)
 
 
 if __name__ == "__main__":

@@ -255,7 +255,7 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
         g->v_lo = std::min<int64_t>((int64_t)rank * g->chunk, nv);
         g->nv = std::min<int64_t>(g->chunk, nv - g->v_lo);
     } else {
-        g->chunk = nv;
+        g->chunk = (nv + 63) / 64 * 64; // whole bitmap words, like the partitioned case
         g->v_lo = 0;
         g->nv = nv;
     }

@@ -766,7 +766,7 @@ int ws_alloc(bfsx_graph *g) {
     ws->nv = g->nv;
     // a partitioned graph pads every rank's slice to chunk/64 words so that frontier slices
     // all-gather into one global bitmap
-    ws->nwords = g->nranks > 1 ? g->chunk / 64 : (g->nv + 63) / 64;
+    ws->nwords = g->chunk / 64;
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
     BFSX_HIP_TRY(hipMalloc(&ws->dist, nv * sizeof(int32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->parent, nv * sizeof(int32_t)));
