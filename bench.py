@@ -97,8 +97,29 @@ def common_fields(args, world, value, wall, nv, m, nnz, nroots, parallelism):
     }
 
 
+def measured_traffic(kernel="k_bu"):
+    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary (profiles/<tag>_hbm.json,
+    written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes),
+    used only while kernels_bfs.hip still hashes to the source it was measured on."""
+    import glob
+    import hashlib
+    src = os.path.join(PKG, "csrc", "kernels_bfs.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm.json")), reverse=True):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if rec.get("kernels_bfs_sha") == sha and kernel in rec.get("kernels", {}):
+            k = rec["kernels"][kernel]
+            return {"traffic": round(k["traffic_B"] / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
+                    "traffic_source": os.path.relpath(path, ROOT), "fetch_correction": rec.get("fetch_correction")}
+    return {"traffic": None, "traffic_source": "no PMC summary for this kernel source"}
+
+
 def roofline(bu_bytes, bu_ms, bu_launches, note):
     ach = (bu_bytes / bu_launches) / ((bu_ms / bu_launches) * 1e-3) / 1e9 if bu_launches else 0.0
+    tr = measured_traffic()
     return {
         "bound": "hbm",
         "kernel": "k_bu (bottom-up pull)",
@@ -106,7 +127,10 @@ def roofline(bu_bytes, bu_ms, bu_launches, note):
         "peak": PEAK_HBM_GBS,
         "unit": "GB/s",
         "frac": round(ach / PEAK_HBM_GBS, 4),
-        "traffic": None,
+        "traffic": tr.pop("traffic"),
+        "traffic_unit": "MB per launch (FETCH_SIZE x correction + WRITE_SIZE)",
+        "algorithmic": round(bu_bytes / max(bu_launches, 1) / 1e6, 1),
+        **tr,
         "launches": bu_launches,
         "avg_launch_ms": round(bu_ms / max(bu_launches, 1), 4),
         "note": note,

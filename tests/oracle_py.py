@@ -140,7 +140,13 @@ def csr_bfs(nv, off, col, source):
     return dist, parent
 
 
-def validate(nv, off, col, source, dist, parent):
+def validate(nv, off, col, source, dist, parent, rows_sorted=False):
+    """Graph500 rules + BreadthFirstPaths.check (orc_validate bisects rows, so they are sorted here
+    unless the caller says they already are: device rows are degree-ordered by default)."""
+    if not rows_sorted:
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        rows = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off))
+        col = np.ascontiguousarray(col)[np.lexsort((col, rows))]
     dist = np.ascontiguousarray(dist, dtype=np.int32)
     parent = np.ascontiguousarray(parent, dtype=np.int64)
     return lib().orc_validate(nv, _ptr(off), _ptr(col), source, _ptr(dist), _ptr(parent))
