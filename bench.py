@@ -38,9 +38,13 @@ def load_module(name, file):
 
 def level_bytes(ls, nwords):
     """Algorithmic bytes of one level."""
-    if ls["direction"] == 2:  # bottom-up: visited word read + next word write, row offsets and top1
-        # of the live unvisited candidates, adjacency entries scanned, dist+parent of the found
-        return 16 * nwords + 12 * max(ls["unvisited_in"], 0) + 4 * ls["scanned"] + 8 * ls["frontier_out"]
+    if ls["direction"] == 2:  # bottom-up: visited word read + next word write, top1 of every live
+        # candidate, the uint32 offset pair of each row walked past top1 (`claims` counts them), the
+        # adjacency entries walked, the packed state word of every vertex found.  Frontier-bit probes
+        # are not counted: the 8 MiB bitmap is cache-resident.
+        walked = max(ls["scanned"] - ls["unvisited_in"], 0)
+        return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 8 * ls["claims"] + 4 * walked
+                + 8 * ls["frontier_out"])
     # top-down: queue read, row offsets (2 x 8 B per frontier vertex), adjacency rows, winners'
     # dist+parent writes, queue append, degree lookups of the winners
     return 20 * ls["frontier_in"] + 4 * max(ls["mf_in"], 0) + 28 * ls["frontier_out"]

@@ -9,8 +9,12 @@
 //                      device counter slot, read back as one small D2H per level
 //   (no reference analogue)                                          -> K5 bottom-up pull (k_bu) with
 //                      Beamer's direction-optimising switch
-// State: dist int32[n] (INT32_MAX = WHITE), parent int32[n], visited bitmap u64[n/64] (BLACK|GRAY,
-// pre-set for isolated vertices), frontier as a queue u32[] (top-down) or a bitmap u64[] (bottom-up).
+// State: one packed 64-bit word per vertex, st[v] = parent << 32 | dist (dist INT32_MAX = WHITE, the
+// reference's Integer.MAX_VALUE; parent 0xFFFFFFFF = none), so a discovery is ONE 8-byte store instead
+// of two scattered 4-byte stores; the visited bitmap u64[n/64] (BLACK|GRAY, pre-set for isolated
+// vertices); the frontier as a queue u32[] (top-down) or a bitmap u64[] (bottom-up).
+// Row offsets are read as uint32 when the graph's adjacency has < 2^32 entries (half the bytes of the
+// int64 CSR offsets on every vertex probe), as int64 otherwise; every traversal kernel is templated on it.
 #include <algorithm>
 #include <chrono>
 #include <type_traits>
@@ -21,48 +25,57 @@ namespace bfsx {
 
 namespace {
 
+using u64 = unsigned long long;
+
 constexpr int kBS = 256;
 constexpr int kWaves = kBS / 64;
 constexpr int kShards = 64; // stat counters are spread over 64 lines: a single device-scope counter hit
                             // by every workgroup costs ~12 ns per arrival (MI355X_MICROARCH fan-in row)
+constexpr u64 kUnreached = 0xFFFFFFFF7FFFFFFFull; // parent = 0xFFFFFFFF (-1), dist = INT32_MAX
+
+__device__ __host__ inline u64 pack_state(uint32_t parent, int32_t d) { return ((u64)parent << 32) | (uint32_t)d; }
 
 struct alignas(64) StatShard {
-    unsigned long long nf;      // vertices in the produced frontier (bottom-up)
-    unsigned long long mf;      // sum of their degrees (Beamer m_f)
-    unsigned long long scanned; // adjacency entries read (bottom-up; algorithmic-bytes accounting)
-    unsigned long long claims;  // top-down atomicOr claims attempted (diagnostics)
-    unsigned long long pad[4];
+    u64 nf;      // vertices in the produced frontier (bottom-up)
+    u64 mf;      // sum of their degrees (Beamer m_f; top-down levels and the multi-GPU bottom-up step)
+    u64 scanned; // adjacency entries read (algorithmic-bytes accounting)
+    u64 claims;  // top-down atomicOr claims attempted (diagnostics)
+    u64 mu;      // bottom-up: degree sum of the candidates left unvisited (Beamer m_u, exact)
+    u64 pad[3];
 };
+constexpr int kStatFields = 5;
 
 // Counters of one level.  Level L reads slot L%3 (its own frontier, already on the host), accumulates
 // the frontier it produces into slot (L+1)%3 and zeroes slot (L+2)%3: no per-level memset.
 struct LevelSlot {
-    unsigned long long qtail; // top-down next-queue allocation cursor (= frontier size produced)
-    unsigned long long nhub;  // top-down hub-list length
-    unsigned long long pad[6];
+    u64 qtail; // top-down next-queue allocation cursor (= frontier size produced)
+    u64 nhub;  // top-down hub-list length
+    u64 pad[6];
     StatShard sh[kShards];
 };
-constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(unsigned long long));
+constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(u64));
 
 } // namespace
 
 struct BfsWorkspace {
     int64_t nv = 0, nwords = 0;
-    int32_t *dist = nullptr, *parent = nullptr;
-    unsigned long long *vis = nullptr, *front = nullptr, *next = nullptr;
-    unsigned long long *dead = nullptr; // isolated vertices + padding (initial visited bitmap)
+    u64 *st = nullptr;                  // packed parent << 32 | dist
+    uint32_t *off32 = nullptr;          // uint32 copy of the row offsets (nnz < 2^32), else null
+    u64 *vis = nullptr, *front = nullptr, *next = nullptr;
+    u64 *dead = nullptr;                // isolated vertices + padding (initial visited bitmap)
     int64_t n_dead = 0;                 // isolated vertices (excluding padding)
-    uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex
+    uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex (+ kDeg1 flag)
+    uint32_t top1_flag = 0;             // kDeg1 when every global id < 2^31, else 0 (flag unused)
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
     LevelSlot *ring = nullptr;          // device, 3 slots
     LevelSlot *h_slot = nullptr;        // pinned host mirror of one slot
-    unsigned long long *d_cursor = nullptr; // bitmap -> queue compaction cursor
-    unsigned long long *d_red = nullptr;    // reductions (m_comp, reached)
+    u64 *d_cursor = nullptr;            // bitmap -> queue compaction cursor
+    u64 *d_red = nullptr;               // reductions (m_comp, reached)
     int64_t prev_source = -1;
     // multi-GPU level state (bfsx_dist_*)
-    unsigned long long *remote = nullptr, *sendbuf_tmp = nullptr; // unbucketed remote pairs
+    u64 *remote = nullptr;              // unbucketed remote pairs
     int64_t remote_cap = 0;
-    unsigned long long *d_dist_ctr = nullptr; // [0] remote tail, [1..kMaxRanks] count, [...] cursor
+    u64 *d_dist_ctr = nullptr;          // [0] remote tail, [1..kMaxRanks] count, [...] cursor
     int d_level = 0, d_dir = BFSX_DIR_TOPDOWN;
     bool d_in_queue = true;
     int64_t d_nf = 0, d_mf = 0;
@@ -84,7 +97,7 @@ __device__ inline uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
-__device__ inline unsigned long long wave_sum(unsigned long long x) {
+__device__ inline u64 wave_sum(u64 x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
     return x;
@@ -92,47 +105,40 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
 
 __device__ inline void zero_slot(LevelSlot *ring, int level) {
     if (blockIdx.x == 0) {
-        unsigned long long *p = reinterpret_cast<unsigned long long *>(ring + (level + 2) % 3);
+        u64 *p = reinterpret_cast<u64 *>(ring + (level + 2) % 3);
         for (int i = threadIdx.x; i < kSlotWords; i += kBS) p[i] = 0ull;
     }
 }
 
-// Block-uniform: reduce four per-thread values over the workgroup, lane 0 of wave 0 adds them to
-// this workgroup's shard of the level's counters.
-__device__ inline void shard_add(LevelSlot *slot, unsigned long long nf, unsigned long long mf,
-                                 unsigned long long scanned, unsigned long long claims) {
-    __shared__ unsigned long long s_red[4][kWaves];
-    nf = wave_sum(nf);
-    mf = wave_sum(mf);
-    scanned = wave_sum(scanned);
-    claims = wave_sum(claims);
+// Block-uniform: reduce the per-thread stat values over the workgroup; threads 0..4 add them to this
+// workgroup's shard of the level's counters.  Order: nf, mf, scanned, claims, mu.
+__device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu) {
+    __shared__ u64 s_red[kStatFields][kWaves];
+    u64 v[kStatFields] = {nf, mf, scanned, claims, mu};
     const unsigned wave = threadIdx.x >> 6;
-    if (lane_id() == 0) {
-        s_red[0][wave] = nf;
-        s_red[1][wave] = mf;
-        s_red[2][wave] = scanned;
-        s_red[3][wave] = claims;
+#pragma unroll
+    for (int f = 0; f < kStatFields; f++) {
+        v[f] = wave_sum(v[f]);
+        if (lane_id() == 0) s_red[f][wave] = v[f];
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
-        unsigned long long t = 0;
+    if (threadIdx.x < kStatFields) {
+        u64 t = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; w++) t += s_red[threadIdx.x][w];
-        if (t) atomicAdd(reinterpret_cast<unsigned long long *>(&slot->sh[blockIdx.x % kShards]) + threadIdx.x, t);
+        if (t) atomicAdd(reinterpret_cast<u64 *>(&slot->sh[blockIdx.x % kShards]) + threadIdx.x, t);
     }
 }
 
 // ---- K2: source init (after the visited bitmap is reset to the dead mask) -------------------------
 // s: local row of the source (0xFFFFFFFF: the source is owned by another rank); sglob: its global id.
-__global__ void k_init_source(uint32_t s, uint32_t sglob, int64_t prev, const unsigned long long *__restrict__ dead,
-                              int32_t *dist, int32_t *parent, unsigned long long *vis, uint32_t *q,
-                              LevelSlot *ring) {
+__global__ void k_init_source(uint32_t s, uint32_t sglob, int64_t prev, const u64 *__restrict__ dead, u64 *stt,
+                              u64 *vis, uint32_t *q, LevelSlot *ring) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         // a previous isolated source is pre-visited (dead mask) so k_finalize never resets it
-        if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) dist[prev] = INT32_MAX;
+        if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) stt[prev] = kUnreached;
         if (s != 0xFFFFFFFFu) {
-            dist[s] = 0;
-            parent[s] = (int32_t)sglob;
+            stt[s] = pack_state(sglob, 0);
             vis[s >> 6] |= 1ull << (s & 63u);
             q[0] = s;
         }
@@ -155,7 +161,7 @@ struct BlockQueue {
 
 // All 64 lanes of every wave call this (wave-uniform control flow).
 __device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
-    const unsigned long long mask = __ballot(win);
+    const u64 mask = __ballot(win);
     if (mask == 0) return;
     const unsigned lane = lane_id();
     const int leader = __ffsll((long long)mask) - 1;
@@ -169,7 +175,7 @@ __device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
 __device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn) {
     const uint32_t n = q.n;
     if (n == 0) return;
-    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(&cn->qtail, (unsigned long long)n);
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(&cn->qtail, (u64)n);
     __syncthreads();
     const uint32_t gb = q.gbase;
     for (uint32_t i = threadIdx.x; i < n; i += kBS) qout[gb + i] = q.buf[i];
@@ -195,9 +201,9 @@ __device__ inline void bq_init(BlockQueue &q) {
 constexpr int kItems = 4;
 constexpr int kHubBatch = 1024;
 
-__device__ inline bool claim(uint32_t v, unsigned long long *vis, unsigned long long &attempts) {
-    const unsigned long long bit = 1ull << (v & 63u);
-    unsigned long long *w = vis + (v >> 6);
+__device__ inline bool claim(uint32_t v, u64 *vis, u64 &attempts) {
+    const u64 bit = 1ull << (v & 63u);
+    u64 *w = vis + (v >> 6);
     if (*w & bit) return false; // bits are only ever set: a stale line can only under-report
     attempts++;
     return !(atomicOr(w, bit) & bit);
@@ -210,20 +216,20 @@ struct Part {
     uint32_t chunk;  // ids per rank (multiple of 64)
     uint32_t rank;
     uint32_t pad;
-    unsigned long long *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
-    unsigned long long *remote_tail; // their allocation cursor
+    u64 *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
+    u64 *remote_tail; // their allocation cursor
 };
 
 // Remote pairs, LDS-buffered like the local queue (multi-GPU path only).
 constexpr int kRCap = 2048;
 struct RemoteQueue {
-    unsigned long long buf[kRCap];
+    u64 buf[kRCap];
     uint32_t n;
     uint32_t gbase;
 };
 
-__device__ inline void rq_push(RemoteQueue &q, bool send, unsigned long long pair) {
-    const unsigned long long mask = __ballot(send);
+__device__ inline void rq_push(RemoteQueue &q, bool send, u64 pair) {
+    const u64 mask = __ballot(send);
     if (mask == 0) return;
     const unsigned lane = lane_id();
     const int leader = __ffsll((long long)mask) - 1;
@@ -236,7 +242,7 @@ __device__ inline void rq_push(RemoteQueue &q, bool send, unsigned long long pai
 __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
     const uint32_t n = q.n;
     if (n == 0) return;
-    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(pt.remote_tail, (unsigned long long)n);
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(pt.remote_tail, (u64)n);
     __syncthreads();
     const uint32_t gb = q.gbase;
     for (uint32_t i = threadIdx.x; i < n; i += kBS) pt.remote[gb + i] = q.buf[i];
@@ -247,14 +253,12 @@ __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
 
 // Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries; u = local row id)
 // in steps of kBS*kItems.  Block-uniform.  kDist: targets owned by another rank become remote pairs.
-template <bool kDist, class ScanT>
+template <bool kDist, class OffT, class ScanT>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
-                                      uint64_t x_begin, uint64_t x_end, const int64_t *__restrict__ row_off,
-                                      const uint32_t *__restrict__ col, unsigned long long *vis,
-                                      int32_t *__restrict__ dist, int32_t *__restrict__ parent, int32_t nd,
-                                      BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn, const Part &pt,
-                                      RemoteQueue *rq, unsigned long long &acc_mf,
-                                      unsigned long long &attempts) {
+                                      uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
+                                      const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
+                                      int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn,
+                                      const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -285,12 +289,11 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
             }
             if (valid[k] && !send && claim(vl, vis, attempts)) {
                 win = true;
-                dist[vl] = nd;
-                parent[vl] = (int32_t)pu[k];
-                acc_mf += (unsigned long long)(row_off[vl + 1] - row_off[vl]);
+                stt[vl] = pack_state(pu[k], nd);
+                acc_mf += (u64)(row_off[vl + 1] - row_off[vl]);
             }
             bq_push(q, win, vl);
-            if (kDist) rq_push(*rq, send, ((unsigned long long)v[k] << 32) | pu[k]);
+            if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
         }
         __syncthreads();
         if (q.n > (uint32_t)(kQCap - kBS * kItems)) bq_flush(q, qout, cn);
@@ -298,11 +301,10 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
     }
 }
 
-template <bool kDist>
-__global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
+template <bool kDist, class OffT>
+__global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
-                                            uint32_t *__restrict__ qout, unsigned long long *vis,
-                                            int32_t *__restrict__ dist, int32_t *__restrict__ parent,
+                                            uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
                                             LevelSlot *ring, int level, uint32_t hub_deg,
                                             uint32_t *__restrict__ hubs, Part pt) {
     LevelSlot *cn = ring + (level + 1) % 3;
@@ -318,15 +320,15 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
     if (kDist && threadIdx.x == 0) rq->n = 0;
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    unsigned long long acc_mf = 0, attempts = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0;
     for (uint32_t base = blockIdx.x * kBS; base < qlen; base += gridDim.x * kBS) {
         const uint32_t i = base + tid;
         uint32_t deg = 0, u = 0;
         int64_t beg = 0;
         if (i < qlen) {
             u = qin[i];
-            beg = row_off[u];
-            int64_t d = row_off[u + 1] - beg;
+            beg = (int64_t)row_off[u];
+            int64_t d = (int64_t)row_off[u + 1] - beg;
             if (d > (int64_t)hub_deg) {
                 hubs[atomicAdd(&cn->nhub, 1ull)] = u;
                 d = 0;
@@ -346,28 +348,30 @@ __global__ __launch_bounds__(kBS) void k_td(const int64_t *__restrict__ row_off,
         s_scan[tid] = woff + inc - deg;
         s_beg[tid] = beg;
         s_u[tid] = u;
-        if (tid == 0) s_scan[kBS] = total;
+        if (tid == 0) {
+            s_scan[kBS] = total;
+            scanned += total;
+        }
         __syncthreads();
-        sweep_segments<kDist>(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, dist, parent, nd, q, qout, cn,
-                              pt, rq, acc_mf, attempts);
+        sweep_segments<kDist>(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, stt, nd, q, qout, cn, pt, rq,
+                              acc_mf, attempts);
         __syncthreads();
     }
     bq_flush(q, qout, cn);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, 0, attempts);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0);
 }
 
-template <bool kDist>
-__global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row_off,
-                                                 const uint32_t *__restrict__ col,
+template <bool kDist, class OffT>
+__global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
-                                                 unsigned long long *vis, int32_t *__restrict__ dist,
-                                                 int32_t *__restrict__ parent, LevelSlot *ring, int level, Part pt) {
+                                                 u64 *vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
+                                                 Part pt) {
     LevelSlot *cn = ring + (level + 1) % 3;
-    __shared__ unsigned long long s_scan[kHubBatch + 1];
+    __shared__ u64 s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
-    __shared__ unsigned long long s_tsum[kBS];
+    __shared__ u64 s_tsum[kBS];
     __shared__ BlockQueue q;
     __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
@@ -377,20 +381,20 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x;
     constexpr int kPer = kHubBatch / kBS;
-    unsigned long long acc_mf = 0, attempts = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0;
     __syncthreads();
     for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
         const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
         // thread tid owns batch entries [tid*kPer, tid*kPer+kPer): load degrees, local sum
-        unsigned long long d[kPer], local = 0;
+        u64 d[kPer], local = 0;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int idx = (int)tid * kPer + k;
             d[k] = 0;
             if (idx < hb) {
                 const uint32_t u = hubs[h0 + idx];
-                const int64_t b = row_off[u];
-                d[k] = (unsigned long long)(row_off[u + 1] - b);
+                const int64_t b = (int64_t)row_off[u];
+                d[k] = (u64)((int64_t)row_off[u + 1] - b);
                 s_beg[idx] = b;
                 s_u[idx] = u;
             }
@@ -400,13 +404,13 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row
         __syncthreads();
         // block inclusive scan of the per-thread sums (Hillis-Steele in LDS)
         for (int off = 1; off < kBS; off <<= 1) {
-            const unsigned long long add = tid >= (unsigned)off ? s_tsum[tid - off] : 0ull;
+            const u64 add = tid >= (unsigned)off ? s_tsum[tid - off] : 0ull;
             __syncthreads();
             s_tsum[tid] += add;
             __syncthreads();
         }
-        unsigned long long run = s_tsum[tid] - local;
-        const unsigned long long total = s_tsum[kBS - 1];
+        u64 run = s_tsum[tid] - local;
+        const u64 total = s_tsum[kBS - 1];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int idx = (int)tid * kPer + k;
@@ -417,39 +421,39 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const int64_t *__restrict__ row
         __syncthreads();
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
-        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, dist, parent, nd, q, qout,
-                              cn, pt, rq, acc_mf, attempts);
+        if (tid == 0) scanned += x_end - x_begin;
+        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, cn, pt,
+                              rq, acc_mf, attempts);
         __syncthreads();
     }
     bq_flush(q, qout, cn);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, 0, attempts);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0);
 }
 
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
-__global__ __launch_bounds__(kBS) void k_claim_remote(const unsigned long long *__restrict__ pairs, uint32_t npairs,
-                                                      const int64_t *__restrict__ row_off,
-                                                      unsigned long long *vis, int32_t *__restrict__ dist,
-                                                      int32_t *__restrict__ parent, uint32_t *__restrict__ qout,
+template <class OffT>
+__global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pairs, uint32_t npairs,
+                                                      const OffT *__restrict__ row_off, u64 *vis,
+                                                      u64 *__restrict__ stt, uint32_t *__restrict__ qout,
                                                       LevelSlot *ring, int level, uint32_t lo) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ BlockQueue q;
     bq_init(q);
     __syncthreads();
     const int32_t nd = level + 1;
-    unsigned long long acc_mf = 0, attempts = 0;
+    u64 acc_mf = 0, attempts = 0;
     for (uint32_t i0 = blockIdx.x * kBS; i0 < npairs; i0 += gridDim.x * kBS) {
         const uint32_t i = i0 + threadIdx.x;
         bool win = false;
         uint32_t vl = 0;
         if (i < npairs) {
-            const unsigned long long pr = pairs[i];
+            const u64 pr = pairs[i];
             vl = (uint32_t)(pr >> 32) - lo;
             if (claim(vl, vis, attempts)) {
                 win = true;
-                dist[vl] = nd;
-                parent[vl] = (int32_t)(uint32_t)pr;
-                acc_mf += (unsigned long long)(row_off[vl + 1] - row_off[vl]);
+                stt[vl] = pack_state((uint32_t)pr, nd);
+                acc_mf += (u64)(row_off[vl + 1] - row_off[vl]);
             }
         }
         bq_push(q, win, vl);
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const unsigned long long *
         if (q.n > (uint32_t)(kQCap - kBS)) bq_flush(q, qout, cn);
     }
     bq_flush(q, qout, cn);
-    shard_add(cn, 0, acc_mf, 0, attempts);
+    shard_add(cn, 0, acc_mf, 0, attempts, 0);
 }
 
 // Multi-GPU: stable bucketing of remote pairs by owning rank (P <= kMaxRanks).  Two passes over the
@@ -465,9 +469,8 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const unsigned long long *
 // (workgroup, destination) and LDS-ranked scatter.
 constexpr int kMaxRanks = 64;
 
-__global__ __launch_bounds__(kBS) void k_bucket_count(const unsigned long long *__restrict__ pairs, uint64_t n,
-                                                      uint32_t chunk, int nranks,
-                                                      unsigned long long *__restrict__ dcount) {
+__global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, uint64_t n, uint32_t chunk,
+                                                      int nranks, u64 *__restrict__ dcount) {
     __shared__ uint32_t s_h[kMaxRanks];
     for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
     __syncthreads();
@@ -475,21 +478,19 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const unsigned long long *
         atomicAdd(&s_h[(uint32_t)(pairs[i] >> 32) / chunk], 1u);
     __syncthreads();
     for (int d = threadIdx.x; d < nranks; d += kBS)
-        if (s_h[d]) atomicAdd(&dcount[d], (unsigned long long)s_h[d]);
+        if (s_h[d]) atomicAdd(&dcount[d], (u64)s_h[d]);
 }
 
-__global__ __launch_bounds__(kBS) void k_bucket_scatter(const unsigned long long *__restrict__ pairs, uint64_t n,
-                                                        uint32_t chunk, int nranks,
-                                                        const unsigned long long *__restrict__ dcount,
-                                                        unsigned long long *__restrict__ dcursor,
-                                                        unsigned long long *__restrict__ out) {
+__global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, uint64_t n, uint32_t chunk,
+                                                        int nranks, const u64 *__restrict__ dcount,
+                                                        u64 *__restrict__ dcursor, u64 *__restrict__ out) {
     __shared__ uint32_t s_h[kMaxRanks];
-    __shared__ unsigned long long s_base[kMaxRanks];
+    __shared__ u64 s_base[kMaxRanks];
     for (uint64_t i0 = (uint64_t)blockIdx.x * kBS; i0 < n; i0 += (uint64_t)gridDim.x * kBS) {
         for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
         __syncthreads();
         const uint64_t i = i0 + threadIdx.x;
-        unsigned long long pr = 0;
+        u64 pr = 0;
         uint32_t d = 0, r = 0;
         if (i < n) {
             pr = pairs[i];
@@ -499,9 +500,9 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const unsigned long long
         __syncthreads();
         for (int k = threadIdx.x; k < nranks; k += kBS) {
             if (s_h[k]) {
-                unsigned long long off = 0; // exclusive prefix of the destination totals
+                u64 off = 0; // exclusive prefix of the destination totals
                 for (int j = 0; j < k; j++) off += dcount[j];
-                s_base[k] = off + atomicAdd(&dcursor[k], (unsigned long long)s_h[k]);
+                s_base[k] = off + atomicAdd(&dcursor[k], (u64)s_h[k]);
             }
         }
         __syncthreads();
@@ -512,15 +513,26 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const unsigned long long
 
 // ---- K5: bottom-up pull --------------------------------------------------------------------------
 // A wave owns 64 consecutive words of the visited bitmap (4096 vertices): one coalesced 512-B load
-// brings them into registers (lane k holds word w0+k).  The unvisited vertices of the group are then
+// brings them into registers (lane k holds word w0+k).  The unvisited vertices of the group are
 // compacted lane-densely -- a wave prefix of per-word popcounts, a shuffle binary search for the
-// owning word and a popcount bit-select -- so every lane works on a live candidate, whether the
-// level leaves half the vertices unvisited or one in a hundred.  The first probe of a candidate reads
-// top1[v] (its highest-degree neighbour, stored densely: a coalesced wave load for consecutive
-// candidates instead of scattered adjacency lines); only on a miss does the lane walk the rest of
-// its row, four entries per step (independent loads in flight).  Found bits are OR-ed into a
-// per-wave LDS copy of the 64 next-frontier words and written back coalesced with the visited words.
-__device__ inline int select_bit(unsigned long long x, int r) { // position of the r-th set bit (r < popc)
+// owning word and a popcount bit-select -- so every lane works on a live candidate whether the level
+// leaves half the vertices unvisited or one in a hundred.  Then two phases per round of kBuU*64
+// candidates:
+//   A  every lane takes kBuU candidates at once: kBuU coalesced top1[v] loads (v's highest-degree
+//      neighbour), then kBuU independent frontier-bit probes -- the whole round costs two memory
+//      round trips instead of two per candidate.  Hits are done: no row offset is ever read for them.
+//   B  the misses (compacted into LDS with a ballot) walk the rest of their rows, 4 entries per step.
+//      A miss whose row holds only top1 (kDeg1 flag in top1) is settled in A without a row read.
+// Found bits are OR-ed into a per-wave LDS copy of the 64 next-frontier words and written back
+// coalesced with the visited words.  Single GPU: m_f of the new frontier is not needed (a bottom-up
+// level is only ever followed by the n_f test), so the level accumulates the exact m_u instead --
+// the degree sum of the candidates it leaves unvisited, which it reads anyway.  kMf (multi-GPU)
+// also accumulates m_f, the size bound of the next top-down exchange.
+constexpr int kBuU = 4;
+constexpr int kBuRound = 64 * kBuU;
+constexpr uint32_t kDeg1 = 0x80000000u;
+
+__device__ inline int select_bit(u64 x, int r) { // position of the r-th set bit (r < popc)
     int pos = 0;
 #pragma unroll
     for (int half = 32; half >= 1; half >>= 1) {
@@ -534,24 +546,23 @@ __device__ inline int select_bit(unsigned long long x, int r) { // position of t
     return pos;
 }
 
-__global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                            const uint32_t *__restrict__ top1,
-                                            const unsigned long long *__restrict__ front,
-                                            unsigned long long *__restrict__ next,
-                                            unsigned long long *__restrict__ vis, int32_t *__restrict__ dist,
-                                            int32_t *__restrict__ parent, LevelSlot *ring, int level,
-                                            int64_t nwords) {
+template <class OffT, bool kMf>
+__global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                            const uint32_t *__restrict__ top1, const u64 *__restrict__ front,
+                                            u64 *__restrict__ next, u64 *__restrict__ vis, u64 *__restrict__ stt,
+                                            LevelSlot *ring, int level, int64_t nwords, uint32_t fmask) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
-    __shared__ unsigned long long s_nx[kWaves][64];
+    __shared__ u64 s_nx[kWaves][64];
+    __shared__ uint32_t s_miss[kWaves][kBuRound];
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
-    unsigned long long acc_nf = 0, acc_mf = 0, acc_sc = 0;
+    u64 acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0;
     const int64_t wstride = (int64_t)gridDim.x * kWaves * 64;
     for (int64_t w0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; w0 < nwords; w0 += wstride) {
         const int64_t wl = w0 + lane;
-        const unsigned long long vwl = wl < nwords ? vis[wl] : ~0ull;
-        const unsigned long long unv = ~vwl;
+        const u64 vwl = wl < nwords ? vis[wl] : ~0ull;
+        const u64 unv = ~vwl;
         const uint32_t c = (uint32_t)__popcll(unv);
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = __shfl(incl, 63);
@@ -562,72 +573,105 @@ __global__ __launch_bounds__(kBS) void k_bu(const int64_t *__restrict__ row_off,
         const uint32_t excl = incl - c;
         s_nx[wave][lane] = 0ull;
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t t0 = 0; t0 < total; t0 += 64) {
-            const uint32_t idx = t0 + lane;
-            // owning word (largest k with excl[k] <= idx) and bit, computed by every lane (shuffles
-            // need all lanes active); lanes past the end work on a clamped index and are masked below
-            const uint32_t ic = idx < total ? idx : total - 1;
-            int k = 0;
+        const uint32_t vbase = (uint32_t)(w0 * 64);
+        for (uint32_t t0 = 0; t0 < total; t0 += kBuRound) {
+            uint32_t v[kBuU], x[kBuU];
+            u64 fw[kBuU];
 #pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-                const uint32_t e = __shfl(excl, (k + step) & 63);
-                if (k + step < 64 && e <= ic) k += step;
-            }
-            const unsigned long long uk = __shfl(unv, k);
-            const int bit = select_bit(uk, (int)(ic - __shfl(excl, k)));
-            if (idx < total) {
-                const int64_t v = (w0 + k) * 64 + bit; // < nv: padding bits are set in the dead mask
-                const int64_t b = row_off[v], e = row_off[v + 1];
-                const uint32_t x = top1[v];
-                bool found = false;
-                uint32_t par = 0;
-                int64_t j = b + 1;
-                if ((front[x >> 6] >> (x & 63u)) & 1ull) {
-                    found = true;
-                    par = x;
+            for (int k = 0; k < kBuU; k++) {
+                // owning word (largest kk with excl[kk] <= idx) and bit, computed by every lane (shuffles
+                // need all lanes active); lanes past the end work on a clamped index and are masked
+                const uint32_t idx = t0 + (uint32_t)k * 64 + lane;
+                const uint32_t ic = idx < total ? idx : total - 1;
+                int kk = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const uint32_t e = __shfl(excl, (kk + step) & 63);
+                    if (kk + step < 64 && e <= ic) kk += step;
                 }
-                while (!found && j < e) {
-                    const int64_t left = e - j;
-                    const uint32_t x0 = col[j];
-                    const uint32_t x1 = left > 1 ? col[j + 1] : x0;
-                    const uint32_t x2 = left > 2 ? col[j + 2] : x0;
-                    const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                    const bool h0 = (front[x0 >> 6] >> (x0 & 63u)) & 1ull;
-                    const bool h1 = (front[x1 >> 6] >> (x1 & 63u)) & 1ull;
-                    const bool h2 = (front[x2 >> 6] >> (x2 & 63u)) & 1ull;
-                    const bool h3 = (front[x3 >> 6] >> (x3 & 63u)) & 1ull;
-                    if (h0 | h1 | h2 | h3) {
-                        found = true;
-                        const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
-                        par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
-                        j += h + 1;
+                const u64 uk = __shfl(unv, kk);
+                v[k] = vbase + (uint32_t)kk * 64 + (uint32_t)select_bit(uk, (int)(ic - __shfl(excl, kk)));
+            }
+#pragma unroll
+            for (int k = 0; k < kBuU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < total) ? top1[v[k]] : 0u;
+#pragma unroll
+            for (int k = 0; k < kBuU; k++) {
+                const uint32_t id = x[k] & ~fmask;
+                fw[k] = (t0 + (uint32_t)k * 64 + lane < total) ? front[id >> 6] : 0ull;
+            }
+            uint32_t nmiss = 0; // wave-uniform
+#pragma unroll
+            for (int k = 0; k < kBuU; k++) {
+                const bool ok = t0 + (uint32_t)k * 64 + lane < total;
+                const uint32_t id = x[k] & ~fmask;
+                const bool hit = ok && ((fw[k] >> (id & 63u)) & 1ull);
+                const bool last = (x[k] & fmask) != 0; // top1 was the row's only entry
+                if (ok) acc_sc += 1;
+                if (hit) {
+                    stt[v[k]] = pack_state(id, nd);
+                    atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
+                    acc_nf += 1;
+                    if (kMf) acc_mf += (u64)(row_off[v[k] + 1] - row_off[v[k]]);
+                } else if (ok && last) {
+                    acc_mu += 1;
+                }
+                const bool miss = ok && !hit && !last;
+                const u64 mm = __ballot(miss);
+                if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
+                nmiss += (uint32_t)__popcll(mm);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
+                if (m0 + lane < nmiss) {
+                    const uint32_t vv = s_miss[wave][m0 + lane];
+                    const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
+                    bool found = false;
+                    uint32_t par = 0;
+                    int64_t j = b + 1;
+                    while (!found && j < e) {
+                        const int64_t left = e - j;
+                        const uint32_t x0 = col[j];
+                        const uint32_t x1 = left > 1 ? col[j + 1] : x0;
+                        const uint32_t x2 = left > 2 ? col[j + 2] : x0;
+                        const uint32_t x3 = left > 3 ? col[j + 3] : x0;
+                        const bool h0 = (front[x0 >> 6] >> (x0 & 63u)) & 1ull;
+                        const bool h1 = (front[x1 >> 6] >> (x1 & 63u)) & 1ull;
+                        const bool h2 = (front[x2 >> 6] >> (x2 & 63u)) & 1ull;
+                        const bool h3 = (front[x3 >> 6] >> (x3 & 63u)) & 1ull;
+                        if (h0 | h1 | h2 | h3) {
+                            found = true;
+                            const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
+                            par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
+                            j += h + 1;
+                        } else {
+                            j += left < 4 ? left : 4;
+                        }
+                    }
+                    acc_sc += (u64)(j - b - 1);
+                    acc_rows += 1;
+                    if (found) {
+                        stt[vv] = pack_state(par, nd);
+                        atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
+                        acc_nf += 1;
+                        if (kMf) acc_mf += (u64)(e - b);
                     } else {
-                        j += left < 4 ? left : 4;
+                        acc_mu += (u64)(e - b);
                     }
                 }
-                acc_sc += (unsigned long long)(j - b);
-                if (found) {
-                    dist[v] = nd;
-                    parent[v] = (int32_t)par;
-                    atomicOr(&s_nx[wave][k], 1ull << bit);
-                    acc_mf += (unsigned long long)(e - b);
-                    acc_nf += 1;
-                }
             }
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
-        const unsigned long long nxl = s_nx[wave][lane];
+        const u64 nxl = s_nx[wave][lane];
         if (wl < nwords) {
             next[wl] = nxl;
             if (nxl) vis[wl] = vwl | nxl;
         }
     }
-    shard_add(cn, acc_nf, acc_mf, acc_sc, 0);
+    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu); // claims field: rows walked (phase B)
 }
 
 // ---- K4: frontier representation changes -------------------------------------------------------
-__global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restrict__ q, uint32_t qlen,
-                                                         unsigned long long *bm) {
+__global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restrict__ q, uint32_t qlen, u64 *bm) {
     for (uint32_t i = blockIdx.x * kBS + threadIdx.x; i < qlen; i += gridDim.x * kBS) {
         const uint32_t v = q[i];
         atomicOr(bm + (v >> 6), 1ull << (v & 63u));
@@ -640,16 +684,16 @@ __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restr
 // reservation counter sees a few hundred arrivals, not one per wave.
 constexpr int kCompactWords = 16;
 
-__global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const unsigned long long *__restrict__ bm, int64_t nwords,
+__global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const u64 *__restrict__ bm, int64_t nwords,
                                                          int64_t words_per_block, uint32_t *__restrict__ q,
-                                                         unsigned long long *cursor) {
+                                                         u64 *cursor) {
     __shared__ uint32_t s_wsum[kWaves];
     __shared__ uint32_t s_base;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int64_t wb = (int64_t)blockIdx.x * words_per_block;
     const int64_t we = min(nwords, wb + words_per_block);
     for (int64_t w0 = wb; w0 < we; w0 += (int64_t)kBS * kCompactWords) {
-        unsigned long long x[kCompactWords];
+        u64 x[kCompactWords];
         uint32_t c = 0;
 #pragma unroll
         for (int i = 0; i < kCompactWords; i++) {
@@ -666,12 +710,12 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const unsigned long lon
             woff += (w < (int)wave) ? s_wsum[w] : 0u;
             total += s_wsum[w];
         }
-        if (tid == 0) s_base = total ? (uint32_t)atomicAdd(cursor, (unsigned long long)total) : 0u;
+        if (tid == 0) s_base = total ? (uint32_t)atomicAdd(cursor, (u64)total) : 0u;
         __syncthreads();
         uint32_t p = s_base + woff + inc - c;
 #pragma unroll
         for (int i = 0; i < kCompactWords; i++) {
-            unsigned long long y = x[i];
+            u64 y = x[i];
             const int64_t w = w0 + (int64_t)i * kBS + tid;
             while (y) {
                 const int b = __ffsll((long long)y) - 1;
@@ -683,18 +727,31 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const unsigned long lon
     }
 }
 
-// After the last level: vertices left unvisited in this BFS (and not isolated) get INT32_MAX, so the
-// per-BFS init never has to rewrite the whole distance array (isolated vertices keep the INT32_MAX
-// written once when the workspace is created).
-__global__ __launch_bounds__(kBS) void k_finalize(const unsigned long long *__restrict__ vis, int64_t nwords,
-                                                  int32_t *__restrict__ dist) {
+// After the last level: vertices left unvisited in this BFS (and not isolated) become WHITE again
+// (INT32_MAX, no parent), so the per-BFS init never rewrites the whole state array (isolated vertices
+// keep the value written once when the workspace is created).
+__global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ stt) {
     for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
-        unsigned long long u = ~vis[w];
+        u64 u = ~vis[w];
         while (u) {
             const int b = __ffsll((long long)u) - 1;
-            dist[w * 64 + b] = INT32_MAX;
+            stt[w * 64 + b] = kUnreached;
             u &= u - 1ull;
         }
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_fill64(u64 *__restrict__ p, int64_t n, u64 val) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) p[i] = val;
+}
+
+// Result extraction (outside the timed region): packed state -> int32 dist + int32 parent.
+__global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, int64_t n, int32_t *__restrict__ dist,
+                                                int32_t *__restrict__ parent) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        const u64 s = stt[i];
+        dist[i] = (int32_t)(uint32_t)s;
+        parent[i] = (int32_t)(uint32_t)(s >> 32);
     }
 }
 
@@ -703,7 +760,7 @@ __global__ __launch_bounds__(kBS) void k_finalize(const unsigned long long *__re
 // groups that hold only visited/isolated vertices with one uniform branch.
 __global__ __launch_bounds__(kBS) void k_dead_mask(const int64_t *__restrict__ row_off,
                                                    const uint32_t *__restrict__ col, int64_t nv, int64_t nwords,
-                                                   uint32_t lo, unsigned long long *__restrict__ dead) {
+                                                   uint32_t lo, u64 *__restrict__ dead) {
     const unsigned lane = lane_id();
     for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords;
          w += ((int64_t)gridDim.x * kBS) >> 6) {
@@ -713,34 +770,40 @@ __global__ __launch_bounds__(kBS) void k_dead_mask(const int64_t *__restrict__ r
             const int64_t b = row_off[v], e = row_off[v + 1];
             d = (e == b) || (e == b + 1 && col[b] == (uint32_t)(v + lo));
         }
-        const unsigned long long m = __ballot(d);
+        const u64 m = __ballot(d);
         if (lane == 0) dead[w] = m;
     }
 }
 
+// top1[v] = first (highest-degree) neighbour, flagged with `flag` when it is the row's only entry.
 __global__ __launch_bounds__(kBS) void k_top1(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                              int64_t nv, uint32_t *__restrict__ top1) {
+                                              int64_t nv, uint32_t flag, uint32_t *__restrict__ top1) {
     for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
-        const int64_t b = row_off[v];
-        top1[v] = (row_off[v + 1] > b) ? col[b] : (uint32_t)v;
+        const int64_t b = row_off[v], e = row_off[v + 1];
+        top1[v] = (e > b) ? (col[b] | (e == b + 1 ? flag : 0u)) : (uint32_t)v;
     }
 }
 
-__global__ __launch_bounds__(kBS) void k_popc(const unsigned long long *__restrict__ bm, int64_t nwords,
-                                              unsigned long long *out) {
-    unsigned long long c = 0;
+__global__ __launch_bounds__(kBS) void k_off32(const int64_t *__restrict__ row_off, int64_t n,
+                                               uint32_t *__restrict__ off32) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS)
+        off32[i] = (uint32_t)row_off[i];
+}
+
+__global__ __launch_bounds__(kBS) void k_popc(const u64 *__restrict__ bm, int64_t nwords, u64 *out) {
+    u64 c = 0;
     for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
-        c += (unsigned long long)__popcll(bm[w]);
+        c += (u64)__popcll(bm[w]);
     c = wave_sum(c);
     if (lane_id() == 0 && c) atomicAdd(out, c);
 }
 
 // m_comp (Graph500 TEPS numerator) and reached count, outside the timed region.
-__global__ __launch_bounds__(kBS) void k_mcomp(const int32_t *__restrict__ dist, const uint32_t *__restrict__ tcnt,
-                                               int64_t nv, unsigned long long *out) {
-    unsigned long long m = 0, r = 0;
+__global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, const uint32_t *__restrict__ tcnt,
+                                               int64_t nv, u64 *out) {
+    u64 m = 0, r = 0;
     for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
-        if (dist[v] != INT32_MAX) {
+        if ((int32_t)(uint32_t)stt[v] != INT32_MAX) {
             m += tcnt[v];
             r += 1;
         }
@@ -768,45 +831,122 @@ int ws_alloc(bfsx_graph *g) {
     // all-gather into one global bitmap
     ws->nwords = g->chunk / 64;
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
-    BFSX_HIP_TRY(hipMalloc(&ws->dist, nv * sizeof(int32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ws->parent, nv * sizeof(int32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(unsigned long long)));
-    BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(unsigned long long)));
-    BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(unsigned long long)));
-    BFSX_HIP_TRY(hipMalloc(&ws->dead, ws->nwords * sizeof(unsigned long long)));
+    BFSX_HIP_TRY(hipMalloc(&ws->st, nv * sizeof(u64)));
+    BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(u64)));
+    BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(u64)));
+    BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(u64)));
+    BFSX_HIP_TRY(hipMalloc(&ws->dead, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->qa, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->qb, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->hubs, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->top1, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->ring, 3 * sizeof(LevelSlot)));
     BFSX_HIP_TRY(hipHostMalloc(&ws->h_slot, sizeof(LevelSlot), hipHostMallocDefault));
-    BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(unsigned long long)));
-    BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(unsigned long long)));
+    BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(u64)));
+    BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(u64)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_end));
-    BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ws->dist, 0x7FFFFFFF, nv, st));
-    hipLaunchKernelGGL(k_top1, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, g->d_row_off,
-                       g->d_col, g->nv, ws->top1);
+    const unsigned gfill = clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192);
+    hipLaunchKernelGGL(k_fill64, dim3(gfill), dim3(kBS), 0, st, ws->st, (int64_t)nv, kUnreached);
+    BFSX_HIP_TRY(hipGetLastError());
+    if (g->nnz < (int64_t)0xFFFFFFFFll) { // every offset (incl. row_off[nv] = nnz) fits in uint32
+        BFSX_HIP_TRY(hipMalloc(&ws->off32, (nv + 1) * sizeof(uint32_t)));
+        hipLaunchKernelGGL(k_off32, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv + 1, ws->off32);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    ws->top1_flag = (g->nv_global <= ((int64_t)1 << 31)) ? kDeg1 : 0u;
+    hipLaunchKernelGGL(k_top1, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->d_col, g->nv, ws->top1_flag, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
                        g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
     BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(unsigned long long), st));
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
     hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
                        ws->nwords, ws->d_red);
     BFSX_HIP_TRY(hipGetLastError());
-    unsigned long long nd = 0;
+    u64 nd = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     ws->n_dead = (int64_t)nd - (ws->nwords * 64 - g->nv); // minus padding bits
     return BFSX_OK;
 }
 
+// ---- launch helpers: one per traversal kernel, dispatching on the row-offset width -------------
+template <bool kDist>
+int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int level, const Part &pt) {
+    hipStream_t st = g->ctx->stream;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    const uint32_t hub_deg = g->ctx->opt.hub_degree;
+    const dim3 grid(clamp_grid((nf + kBS - 1) / kBS, cap));
+    // hubs: sized by the frontier's degree sum when known (mf < 0: after a bottom-up level)
+    const bool hubs = mf < 0 || mf > (int64_t)hub_deg;
+    const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
+    if (ws->off32) {
+        hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
+                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt);
+        BFSX_HIP_TRY(hipGetLastError());
+        if (hubs) {
+            hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt);
+            BFSX_HIP_TRY(hipGetLastError());
+        }
+    } else {
+        hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt);
+        BFSX_HIP_TRY(hipGetLastError());
+        if (hubs) {
+            hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt);
+            BFSX_HIP_TRY(hipGetLastError());
+        }
+    }
+    return BFSX_OK;
+}
+
+template <bool kMf>
+int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
+    hipStream_t st = g->ctx->stream;
+    // persistent grid: exactly the resident workgroups (a partial second wave of workgroups would
+    // leave most CUs idle at the tail of the grid-stride loop)
+    static int per_cu = 0;
+    if (!per_cu) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<uint32_t, kMf>, kBS, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 4;
+    }
+    const unsigned cap = (unsigned)(g->ctx->num_cus * per_cu);
+    const dim3 grid(clamp_grid((ws->nwords + kWaves * 64 - 1) / (kWaves * 64), cap));
+    if (ws->off32)
+        hipLaunchKernelGGL((k_bu<uint32_t, kMf>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->top1, front,
+                           ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag);
+    else
+        hipLaunchKernelGGL((k_bu<int64_t, kMf>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->top1, front,
+                           ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag);
+    BFSX_HIP_TRY(hipGetLastError());
+    return BFSX_OK;
+}
+
+struct SlotSums {
+    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0;
+};
+
+SlotSums sum_slot(const LevelSlot *s) {
+    SlotSums r;
+    for (int i = 0; i < kShards; i++) {
+        r.nf += (int64_t)s->sh[i].nf;
+        r.mf += (int64_t)s->sh[i].mf;
+        r.sc += (int64_t)s->sh[i].scanned;
+        r.cl += (int64_t)s->sh[i].claims;
+        r.mu += (int64_t)s->sh[i].mu;
+    }
+    return r;
+}
+
 } // namespace
 
 void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
-    for (void *p : {(void *)ws->dist, (void *)ws->parent, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
+    for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
                     (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr})
@@ -837,16 +977,16 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
 
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
-    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, nwords * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, (uint32_t)source, (uint32_t)source, ws->prev_source, ws->dead,
-                       ws->dist, ws->parent, ws->vis, ws->qa, ws->ring);
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, (uint32_t)source, (uint32_t)source, ws->prev_source,
+                       ws->dead, ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
     ws->prev_source = source;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     bool in_queue = true; // frontier currently held in ws->qa (else in ws->front)
     int64_t nf = 1, prev_nf = 0;
-    int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded
+    int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded (-1: unknown)
     int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
@@ -871,13 +1011,13 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
         if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
-            BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(unsigned long long), st));
+            BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
             hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
                                ws->qa, (uint32_t)nf, ws->front);
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue) {
-            BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(unsigned long long), st));
+            BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
             const int64_t per_block_min = (int64_t)kBS * kCompactWords;
             const unsigned gb = clamp_grid((nwords + per_block_min - 1) / per_block_min, 256);
             const int64_t wpb = ((nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
@@ -888,60 +1028,47 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         }
         if (dir == BFSX_DIR_TOPDOWN) {
             const Part pt{};
-            hipLaunchKernelGGL(k_td<false>, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                               g->d_row_off, g->d_col, ws->qa, (uint32_t)nf, ws->qb, ws->vis, ws->dist, ws->parent,
-                               ws->ring, level, opt.hub_degree, ws->hubs, pt);
-            BFSX_HIP_TRY(hipGetLastError());
-            if (mf > (int64_t)opt.hub_degree) { // some frontier vertex may exceed the hub degree
-                const dim3 gh(clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
-                hipLaunchKernelGGL(k_td_hubs<false>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                                   ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level, pt);
-                BFSX_HIP_TRY(hipGetLastError());
-            }
+            if (int e = launch_td<false>(g, ws, nf, mf, level, pt)) return e;
             td_levels++;
         } else {
-            hipLaunchKernelGGL(k_bu, dim3(clamp_grid((nwords + kWaves * 64 - 1) / (kWaves * 64), cap)), dim3(kBS), 0,
-                               st, g->d_row_off, g->d_col, ws->top1, ws->front, ws->next, ws->vis, ws->dist,
-                               ws->parent, ws->ring, level, nwords);
-            BFSX_HIP_TRY(hipGetLastError());
+            if (int e = launch_bu<false>(g, ws, ws->front, level)) return e;
             bu_levels++;
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
         BFSX_HIP_TRY(hipMemcpyAsync(ws->h_slot, ws->ring + (level + 1) % 3, sizeof(LevelSlot), hipMemcpyDeviceToHost,
                                     st));
         BFSX_HIP_TRY(hipStreamSynchronize(st));
-        int64_t s_nf = 0, s_mf = 0, s_sc = 0, s_cl = 0;
-        for (int i = 0; i < kShards; i++) {
-            s_nf += (int64_t)ws->h_slot->sh[i].nf;
-            s_mf += (int64_t)ws->h_slot->sh[i].mf;
-            s_sc += (int64_t)ws->h_slot->sh[i].scanned;
-            s_cl += (int64_t)ws->h_slot->sh[i].claims;
-        }
-        const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? (int64_t)ws->h_slot->qtail : s_nf;
+        const SlotSums s = sum_slot(ws->h_slot);
+        const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? (int64_t)ws->h_slot->qtail : s.nf;
         g->level_dirs.push_back(dir);
         bfsx_level_stat ls{};
         ls.direction = dir;
         ls.level = level;
         ls.frontier_in = nf;
         ls.frontier_out = nf_new;
-        ls.mf_in = mf;
-        ls.unvisited_in = nv - visited - ws->n_dead; // live candidates (isolated ones are pre-visited)
-        ls.scanned = (dir == BFSX_DIR_TOPDOWN) ? mf : s_sc;
-        ls.claims = s_cl;
+        ls.mf_in = (dir == BFSX_DIR_TOPDOWN) ? s.sc : mf; // top-down: the kernels count the rows they sweep
+        ls.unvisited_in = nv - visited - ws->n_dead;      // live candidates (isolated ones are pre-visited)
+        ls.scanned = s.sc;
+        ls.claims = s.cl;
         g->level_stats.push_back(ls);
         examined += ls.scanned;
         visited += nf_new;
-        mu -= s_mf;
         prev_nf = nf;
         nf = nf_new;
-        mf = s_mf;
-        if (dir == BFSX_DIR_TOPDOWN) std::swap(ws->qa, ws->qb);
-        else std::swap(ws->front, ws->next);
+        if (dir == BFSX_DIR_TOPDOWN) {
+            mu -= s.mf;
+            mf = s.mf;
+            std::swap(ws->qa, ws->qb);
+        } else {
+            mu = s.mu; // exact: degree sum of the candidates this level left unvisited
+            mf = -1;   // not accumulated by the single-GPU bottom-up step
+            std::swap(ws->front, ws->next);
+        }
         if (nf == 0) break;
     }
-    // unvisited (non-isolated) vertices -> INT32_MAX; inside the timed region
-    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis,
-                       nwords, ws->dist);
+    // unvisited (non-isolated) vertices -> WHITE; inside the timed region
+    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis, nwords,
+                       ws->st);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
@@ -971,9 +1098,9 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached) {
     BfsWorkspace *ws = g->ws;
     hipStream_t st = g->ctx->stream;
-    unsigned long long h[2] = {0, 0};
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_mcomp, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dist,
+    u64 h[2] = {0, 0};
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(u64), st));
+    hipLaunchKernelGGL(k_mcomp, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->st,
                        g->d_tuple_cnt, g->nv, ws->d_red);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipMemcpyAsync(h, ws->d_red, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -988,19 +1115,19 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     if (!ws || g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
     hipStream_t st = g->ctx->stream;
     const size_t nv = (size_t)g->nv;
-    std::vector<int32_t> dtmp;
-    int32_t *dist = dist_out;
-    if (!dist) {
-        dtmp.resize(nv);
-        dist = dtmp.data();
-    }
-    BFSX_HIP_TRY(hipMemcpyAsync(dist, ws->dist, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    // unpack into the (idle) frontier queues, then D2H
+    int32_t *d_dist = reinterpret_cast<int32_t *>(ws->qa), *d_par = reinterpret_cast<int32_t *>(ws->qb);
+    hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
+                       (int64_t)nv, d_dist, d_par);
+    BFSX_HIP_TRY(hipGetLastError());
+    if (dist_out) BFSX_HIP_TRY(hipMemcpyAsync(dist_out, d_dist, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (parent_out) {
         // int32 device parents land in the upper half of the int64 output, then widen in place
+        // (0xFFFFFFFF = none -> -1)
         int32_t *p32 = reinterpret_cast<int32_t *>(parent_out) + nv;
-        BFSX_HIP_TRY(hipMemcpyAsync(p32, ws->parent, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipMemcpyAsync(p32, d_par, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         BFSX_HIP_TRY(hipStreamSynchronize(st));
-        for (size_t i = 0; i < nv; i++) parent_out[i] = (dist[i] == INT32_MAX) ? -1 : (int64_t)p32[i];
+        for (size_t i = 0; i < nv; i++) parent_out[i] = (int64_t)p32[i];
     } else {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
     }
@@ -1027,8 +1154,7 @@ inline Part make_part(bfsx_graph *g, BfsWorkspace *ws) {
 int dist_ws(bfsx_graph *g) {
     int rc = ws_alloc(g);
     if (rc) return rc;
-    if (!g->ws->d_dist_ctr)
-        BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, (1 + 2 * kMaxRanks) * sizeof(unsigned long long)));
+    if (!g->ws->d_dist_ctr) BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, (1 + 2 * kMaxRanks) * sizeof(u64)));
     return BFSX_OK;
 }
 
@@ -1060,9 +1186,9 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local) {
         deg = so[1] - so[0];
     }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
-    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, ws->nwords * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)source,
-                       ws->prev_source, ws->dead, ws->dist, ws->parent, ws->vis, ws->qa, ws->ring);
+                       ws->prev_source, ws->dead, ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
     ws->prev_source = sl;
     ws->d_level = 0;
@@ -1086,17 +1212,15 @@ int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int 
     return BFSX_OK;
 }
 
-int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, int64_t *send_counts) {
+int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_counts) {
     BfsWorkspace *ws = g->ws;
     if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
     hipStream_t st = g->ctx->stream;
-    const Options &opt = g->ctx->opt;
-    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     const int level = ws->d_level, P = g->nranks;
     if (int rc2 = dist_level_events(ws, level)) return rc2;
     BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
     if (!ws->d_in_queue) { // frontier held as a local bitmap slice (after a bottom-up level)
-        BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(unsigned long long), st));
+        BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
         const int64_t per_block_min = (int64_t)kBS * kCompactWords;
         const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
         const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
@@ -1111,25 +1235,16 @@ int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, 
         if (ws->remote) BFSX_HIP_TRY(hipFree(ws->remote));
         ws->remote = nullptr;
         ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
-        BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(unsigned long long)));
+        BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
     }
     if (send_cap < ws->d_mf) return fail(BFSX_E_ARG, "send buffer smaller than the local frontier's m_f");
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, (1 + 2 * kMaxRanks) * sizeof(unsigned long long), st));
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, (1 + 2 * kMaxRanks) * sizeof(u64), st));
     const Part pt = make_part(g, ws);
-    hipLaunchKernelGGL(k_td<true>, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, g->d_row_off,
-                       g->d_col, ws->qa, (uint32_t)ws->d_nf, ws->qb, ws->vis, ws->dist, ws->parent, ws->ring, level,
-                       opt.hub_degree, ws->hubs, pt);
-    BFSX_HIP_TRY(hipGetLastError());
-    if (ws->d_mf > (int64_t)opt.hub_degree) {
-        const dim3 gh(clamp_grid((ws->d_mf + kBS * kItems - 1) / (kBS * kItems), cap));
-        hipLaunchKernelGGL(k_td_hubs<true>, gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs, ws->qb, ws->vis,
-                           ws->dist, ws->parent, ws->ring, level, pt);
-        BFSX_HIP_TRY(hipGetLastError());
-    }
-    unsigned long long n_remote = 0;
+    if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, level, pt)) return e;
+    u64 n_remote = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&n_remote, ws->d_dist_ctr, sizeof(n_remote), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
-    unsigned long long *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
+    u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
     if (n_remote > 0) {
         const unsigned gbk = clamp_grid(((int64_t)n_remote + kBS - 1) / kBS, 1024);
         hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, (uint64_t)n_remote,
@@ -1139,28 +1254,32 @@ int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, 
                            (uint32_t)g->chunk, P, dcount, dcursor, d_send);
         BFSX_HIP_TRY(hipGetLastError());
     }
-    std::vector<unsigned long long> h(P, 0);
-    BFSX_HIP_TRY(hipMemcpyAsync(h.data(), dcount, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    std::vector<u64> h(P, 0);
+    BFSX_HIP_TRY(hipMemcpyAsync(h.data(), dcount, P * sizeof(u64), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     for (int p = 0; p < P; p++) send_counts[p] = (int64_t)h[p];
     ws->d_dir = BFSX_DIR_TOPDOWN;
     return BFSX_OK;
 }
 
-int dist_td_claim(bfsx_graph *g, const unsigned long long *d_recv, int64_t n) {
+int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     BfsWorkspace *ws = g->ws;
     if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
     if (n <= 0) return BFSX_OK;
     hipStream_t st = g->ctx->stream;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
-    hipLaunchKernelGGL(k_claim_remote, dim3(clamp_grid((n + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, d_recv,
-                       (uint32_t)n, g->d_row_off, ws->vis, ws->dist, ws->parent, ws->qb, ws->ring, ws->d_level,
-                       (uint32_t)g->v_lo);
+    const dim3 grid(clamp_grid((n + kBS - 1) / kBS, cap));
+    if (ws->off32)
+        hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (uint32_t)n, ws->off32, ws->vis,
+                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo);
+    else
+        hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (uint32_t)n, g->d_row_off,
+                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
 
-int dist_frontier_slice(bfsx_graph *g, unsigned long long *d_slice) {
+int dist_frontier_slice(bfsx_graph *g, u64 *d_slice) {
     BfsWorkspace *ws = g->ws;
     if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
     hipStream_t st = g->ctx->stream;
@@ -1168,27 +1287,21 @@ int dist_frontier_slice(bfsx_graph *g, unsigned long long *d_slice) {
     if (int rc2 = dist_level_events(ws, ws->d_level)) return rc2;
     BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[ws->d_level], st));
     if (ws->d_in_queue) {
-        BFSX_HIP_TRY(hipMemsetAsync(d_slice, 0, ws->nwords * sizeof(unsigned long long), st));
+        BFSX_HIP_TRY(hipMemsetAsync(d_slice, 0, ws->nwords * sizeof(u64), st));
         hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
                            ws->qa, (uint32_t)ws->d_nf, d_slice);
         BFSX_HIP_TRY(hipGetLastError());
     } else {
-        BFSX_HIP_TRY(hipMemcpyAsync(d_slice, ws->front, ws->nwords * sizeof(unsigned long long),
-                                    hipMemcpyDeviceToDevice, st));
+        BFSX_HIP_TRY(hipMemcpyAsync(d_slice, ws->front, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
     }
     BFSX_HIP_TRY(hipStreamSynchronize(st)); // the caller hands the slice to a collective next
     return BFSX_OK;
 }
 
-int dist_bu_step(bfsx_graph *g, const unsigned long long *d_front_global) {
+int dist_bu_step(bfsx_graph *g, const u64 *d_front_global) {
     BfsWorkspace *ws = g->ws;
     if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
-    hipStream_t st = g->ctx->stream;
-    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
-    hipLaunchKernelGGL(k_bu, dim3(clamp_grid((ws->nwords + kWaves * 64 - 1) / (kWaves * 64), cap)), dim3(kBS), 0, st,
-                       g->d_row_off, g->d_col, ws->top1, d_front_global, ws->next, ws->vis, ws->dist, ws->parent,
-                       ws->ring, ws->d_level, ws->nwords);
-    BFSX_HIP_TRY(hipGetLastError());
+    if (int e = launch_bu<true>(g, ws, d_front_global, ws->d_level)) return e;
     ws->d_dir = BFSX_DIR_BOTTOMUP;
     ws->d_in_queue = false;
     return BFSX_OK;
@@ -1203,33 +1316,27 @@ int dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local) {
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipMemcpyAsync(ws->h_slot, ws->ring + (level + 1) % 3, sizeof(LevelSlot), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
-    int64_t s_nf = 0, s_mf = 0, s_sc = 0, s_cl = 0;
-    for (int i = 0; i < kShards; i++) {
-        s_nf += (int64_t)ws->h_slot->sh[i].nf;
-        s_mf += (int64_t)ws->h_slot->sh[i].mf;
-        s_sc += (int64_t)ws->h_slot->sh[i].scanned;
-        s_cl += (int64_t)ws->h_slot->sh[i].claims;
-    }
+    const SlotSums s = sum_slot(ws->h_slot);
     const bool td = ws->d_dir == BFSX_DIR_TOPDOWN;
-    const int64_t nf_new = td ? (int64_t)ws->h_slot->qtail : s_nf;
+    const int64_t nf_new = td ? (int64_t)ws->h_slot->qtail : s.nf;
     bfsx_level_stat ls{};
     ls.direction = ws->d_dir;
     ls.level = level;
     ls.frontier_in = ws->d_nf;
     ls.frontier_out = nf_new;
     ls.mf_in = ws->d_mf;
-    ls.scanned = td ? ws->d_mf : s_sc;
-    ls.claims = s_cl;
+    ls.scanned = s.sc;
+    ls.claims = s.cl;
     g->level_stats.push_back(ls);
     g->level_dirs.push_back(ws->d_dir);
     if (td) std::swap(ws->qa, ws->qb);
     else std::swap(ws->front, ws->next);
     ws->d_in_queue = td;
     ws->d_nf = nf_new;
-    ws->d_mf = s_mf;
+    ws->d_mf = s.mf;
     ws->d_level = level + 1;
     *nf_local = nf_new;
-    *mf_local = s_mf;
+    *mf_local = s.mf;
     return BFSX_OK;
 }
 
@@ -1239,7 +1346,7 @@ int dist_finish(bfsx_graph *g) {
     hipStream_t st = g->ctx->stream;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis,
-                       ws->nwords, ws->dist);
+                       ws->nwords, ws->st);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));

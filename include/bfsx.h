@@ -75,7 +75,7 @@ typedef struct bfsx_level_stat {
     int64_t mf_in;         /* sum of frontier degrees (top-down edges scanned) */
     int64_t unvisited_in;  /* WHITE vertices before the pass (bottom-up candidates) */
     int64_t scanned;       /* adjacency entries read (top-down: mf_in; bottom-up: counted) */
-    int64_t claims;        /* top-down: atomic visited-bitmap claims attempted (diagnostics) */
+    int64_t claims;        /* top-down: atomic visited-bitmap claims attempted; bottom-up: rows walked past top1 */
     double kernel_ms;      /* device time of this level's kernels (hipEvents around them) */
     double cum_ms;         /* device time since source init, like the reference's Stopwatch */
 } bfsx_level_stat;
