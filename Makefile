@@ -12,7 +12,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 CXXFLAGS ?= -O2 -std=c++17 -Wall -I include
 
 KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip
-HOST_SRCS   := $(CSRC)/bfsx_api.cpp
+HOST_SRCS   := $(CSRC)/bfsx_api.cpp $(CSRC)/bfsx_comm.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 
 all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark oracle
@@ -26,7 +26,7 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h include/bfsx.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(PKG)/libbfsx.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bfsx_spark: $(HOSTSRC)/bfsx_spark.cpp include/bfsx.h $(PKG)/libbfsx.so
 	$(CXX) $(CXXFLAGS) -o $@ $(HOSTSRC)/bfsx_spark.cpp -L$(PKG) -lbfsx -Wl,-rpath,'$$ORIGIN'

@@ -7,8 +7,9 @@ the K timed roots (= K*m / sum t when every root lies in the giant component).
 
   N = 1: t = device time from source init to the last level (hipEvents inside libbfsx.so).
   N > 1: launched as one process per GPU (torch.distributed.run); the graph is 1-D partitioned over
-         the ranks (bfsx_dist.py) and every level exchanges over RCCL (backend "nccl"); t = the max
-         over ranks of the wall time of one BFS, bracketed by barrier + device synchronise.
+         the ranks and libbfsx runs the level loop with its own RCCL communicator (all-to-allv of
+         owner-routed pairs, all-gather of frontier bitmaps, all-reduce of the level counters);
+         t = the max over ranks of the wall time of one BFS, bracketed by barrier + device sync.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
 
@@ -226,73 +227,73 @@ def run_single(args):
 
 
 def run_dist(args, world, rank, local_rank):
+    """One process per GPU: the partitioned level loop and its RCCL exchange run inside libbfsx
+    (bfsx_dist_bfs); torch.distributed (gloo, host only) is used for the rendezvous -- the RCCL unique
+    id, barriers and the max over ranks of the per-root times -- never on the data path."""
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    dist.init_process_group("nccl")  # RCCL over xGMI
+    dist.init_process_group("gloo")
     bfsx = load_module("bfsx", "bfsx.py")
-    bd = load_module("bfsx_dist", "bfsx_dist.py")
-    opts = dict(kv.split("=", 1) for kv in args.option)
     ctx = bfsx.Context(local_rank, direction=args.direction)
-    for k, val in opts.items():
-        if k not in ("alpha", "beta"):
-            ctx.set_option(k, val)
-    dev = torch.device("cuda", local_rank)
+    for kv in args.option:
+        k, val = kv.split("=", 1)
+        ctx.set_option(k, val)
+    uid = [bfsx.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    ctx.comm_init(rank, world, uid[0])
     t0 = time.perf_counter()
     g = ctx.dist_kronecker(args.scale, rank, world, args.edgefactor, args.seed)
+    ctx.synchronize()
     build_s = time.perf_counter() - t0
-    eng = bd.GpuEngine(torch, g, dev)
-    comm = bd.Comm(torch, dist, dev, staging=False)
-    drv = bd.DistBFS(eng, comm, direction=args.direction, alpha=int(opts.get("alpha", 30)),
-                     beta=int(opts.get("beta", 24)))
-    roots = drv.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)
-    mcomp = {}
-    for r in roots:
-        drv.run(r)
-        mcomp[r] = drv.mcomp()[0]
+    part = g.partition()
+    roots = [int(r) for r in g.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)]
+    mcomp = {r: g.dist_bfs(r)["m_comp"] for r in roots}  # untimed, collective
     order = [roots[i % len(roots)] for i in range(args.warmup + args.steps)]
     for r in order[: args.warmup]:
-        drv.run(r)
+        g.dist_bfs(r, want_stats=False)
 
     def timed(r):
-        torch.cuda.synchronize(dev)
+        ctx.synchronize()
         dist.barrier()
         a = time.perf_counter()
-        drv.run(r)
-        torch.cuda.synchronize(dev)
-        return time.perf_counter() - a
+        dev_ms = g.dist_bfs(r, want_stats=False)
+        ctx.synchronize()
+        return time.perf_counter() - a, dev_ms
 
-    torch.cuda.synchronize(dev)
+    ctx.synchronize()
     dist.barrier()
     w0 = time.perf_counter()
-    local_t = [timed(r) for r in order[args.warmup:]]
-    torch.cuda.synchronize(dev)
+    local = [timed(r) for r in order[args.warmup:]]
+    ctx.synchronize()
     dist.barrier()
     wall = time.perf_counter() - w0
-    tt = torch.tensor(local_t + [wall], dtype=torch.float64, device=dev)
+    tt = torch.tensor([x[0] for x in local] + [wall], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)  # max over ranks, per root
-    t_root = tt[:-1].cpu().tolist()
+    t_root = tt[:-1].tolist()
     wall = float(tt[-1])
     steps_roots = order[args.warmup:]
     gteps = [mcomp[r] / t / 1e9 for r, t in zip(steps_roots, t_root)]
-    nnz = comm.allreduce_i64([g.nnz])[0]
+    nnz = torch.tensor([g.nnz], dtype=torch.int64)
+    dist.all_reduce(nnz)
     if rank == 0:
-        out = common_fields(args, world, hmean(gteps), wall, eng.nv_global, g.m, nnz, len(roots),
-                            f"1d-partition dp{world} (RCCL all-to-all + all-gather)")
+        out = common_fields(args, world, hmean(gteps), wall, part["nv_global"], g.m, int(nnz), len(roots),
+                            f"1d-partition dp{world} (RCCL all-to-allv + all-gather + all-reduce in libbfsx)")
+        out["scaling"] = "strong"
         bu_bytes, bu_ms, bu_launches = 0, 0.0, 0
-        for ls in g.level_stats(256):  # rank 0's last BFS: kernel time incl. the all-gather wait
+        for ls in g.level_stats(256):  # rank 0, last timed BFS
             if ls["direction"] == 2:
-                bu_bytes += level_bytes(dict(ls, unvisited_in=eng.nv_local), eng.slice_words)
+                bu_bytes += level_bytes(ls, part["chunk"] // 64)
                 bu_ms += ls["kernel_ms"]
                 bu_launches += 1
         out["roofline"] = roofline(bu_bytes, bu_ms, bu_launches,
-                                   "rank 0, last BFS; bottom-up level time includes the all-gather wait; "
-                                   "unvisited_in bounded by the local row count")
+                                   "rank 0, last BFS; a bottom-up level's time includes its frontier all-gather")
         out.update({"t_bfs_ms_mean": float(np.mean(t_root)) * 1e3, "t_bfs_ms_min": float(np.min(t_root)) * 1e3,
+                    "t_bfs_dev_ms_rank0_mean": float(np.mean([x[1] for x in local])),
                     "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])),
                     "graph_build_s": round(build_s, 3), "cpu_baseline": None,
-                    "levels_last": drv.level_log})
+                    "levels_last": [{k: ls[k] for k in ("level", "direction", "frontier_in", "frontier_out",
+                                                        "kernel_ms")} for ls in g.level_stats(256)]})
         print(json.dumps(out), flush=True)
     g.free()
     ctx.close()

@@ -37,8 +37,9 @@ EXPORTS = [
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
     "bfsx_dist_begin", "bfsx_dist_frontier_info", "bfsx_dist_td_expand", "bfsx_dist_td_claim",
     "bfsx_dist_frontier_slice", "bfsx_dist_bu_step", "bfsx_dist_level_end", "bfsx_dist_finish",
-    "bfsx_dist_mcomp",
+    "bfsx_dist_mcomp", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group", "bfsx_dist_bfs",
 ]
+COMM_ID_BYTES = 128
 
 
 class Stats(C.Structure):
@@ -117,6 +118,10 @@ def lib():
         L.bfsx_dist_level_end.argtypes = [_VP, I64P, I64P]
         L.bfsx_dist_finish.argtypes = [_VP]
         L.bfsx_dist_mcomp.argtypes = [_VP, I64P, I64P]
+        L.bfsx_comm_unique_id.argtypes = [_VP]
+        L.bfsx_comm_init.argtypes = [_VP, C.c_int, C.c_int, _VP]
+        L.bfsx_comm_local_group.argtypes = [_VP, C.c_int]
+        L.bfsx_dist_bfs.argtypes = [_VP, C.c_int64, C.POINTER(Stats)]
         _lib = L
     return _lib
 
@@ -129,6 +134,20 @@ def _check(rc):
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def comm_unique_id():
+    """RCCL unique id (bytes) for bfsx_comm_init; rank 0 creates it, the caller distributes it."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _check(lib().bfsx_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def local_group(ctxs):
+    """Attach an in-process exchange group to the contexts (rank r = ctxs[r]); each rank must then
+    be driven by its own host thread (bfsx_dist_bfs is collective)."""
+    arr = (_VP * len(ctxs))(*[c._h for c in ctxs])
+    _check(lib().bfsx_comm_local_group(arr, len(ctxs)))
 
 
 def parse_algs4(path):
@@ -197,6 +216,12 @@ class Context:
 
     def synchronize(self):
         _check(lib().bfsx_device_synchronize(self._h))
+
+    def comm_init(self, rank, nranks, uid):
+        """Collective over the nranks processes: attach an RCCL communicator to this context."""
+        assert len(uid) == COMM_ID_BYTES
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        _check(lib().bfsx_comm_init(self._h, rank, nranks, buf))
 
     def close(self):
         if self._h:
@@ -316,6 +341,19 @@ class Graph:
 
     def dist_finish(self):
         _check(lib().bfsx_dist_finish(self._h))
+
+    def dist_bfs(self, source, want_stats=True):
+        """Partitioned BFS, the whole level loop + exchanges in libbfsx (collective: every rank calls
+        it with the same source).  Returns the stats dict (m_comp/reached all-reduced) or the device
+        time in ms when want_stats is False."""
+        if want_stats:
+            st = Stats()
+            _check(lib().bfsx_dist_bfs(self._h, source, C.byref(st)))
+            return st.as_dict()
+        _check(lib().bfsx_dist_bfs(self._h, source, None))
+        buf = np.empty(1 << 16, np.float64)
+        n = lib().bfsx_level_times(self._h, _p(buf), len(buf))
+        return float(buf[n - 1]) if n > 0 else float("nan")
 
     def dist_mcomp(self):
         a, b = C.c_int64(), C.c_int64()

@@ -201,6 +201,7 @@ int bfsx_init(int device, bfsx_ctx **out) {
 void bfsx_finalize(bfsx_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    ctx->comm.reset();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -454,6 +455,11 @@ int bfsx_dist_finish(bfsx_graph *g) {
     return dist_finish(g);
 }
 
+int bfsx_dist_bfs(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
+    BFSX_DIST_GUARD(g);
+    return dist_bfs_run(g, source, stats);
+}
+
 int bfsx_dist_mcomp(bfsx_graph *g, int64_t *m_local, int64_t *reached_local) {
     BFSX_DIST_GUARD(g);
     int64_t a = 0, b = 0;
@@ -492,23 +498,46 @@ int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col) {
 
 int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
     if (!g || !roots || count < 0) return fail(BFSX_E_ARG, "bad argument");
-    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: sample roots with bfsx_graph_degree");
+    // a partitioned graph samples collectively: the owner of each candidate decides, the verdict is
+    // all-reduced, so every rank returns the same roots as the single-device graph would
+    const bool part = g->nranks > 1;
+    Comm *cm = g->ctx->comm.get();
+    if (part && (!cm || cm->nranks != g->nranks || cm->rank != g->rank))
+        return fail(BFSX_E_ARG, "partitioned graph: attach a communicator first (sampling is collective)");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    hipStream_t st = g->ctx->stream;
+    struct DevFlag {
+        int64_t *p = nullptr;
+        ~DevFlag() {
+            if (p) (void)hipFree(p);
+        }
+    } flag;
+    if (part) BFSX_HIP_TRY(hipMalloc(&flag.p, sizeof(int64_t)));
     std::unordered_set<int64_t> seen;
     int found = 0;
     const uint64_t max_tries = 1000ull + 1000ull * (uint64_t)count;
     for (uint64_t t = 0; t < max_tries && found < count; t++) {
-        const int64_t x = (int64_t)(mix64(seed + t) % (uint64_t)g->nv);
+        const int64_t x = (int64_t)(mix64(seed + t) % (uint64_t)g->nv_global);
         if (seen.count(x)) continue;
-        int64_t off[2];
-        BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + x, sizeof(off), hipMemcpyDeviceToHost));
-        const int64_t deg = off[1] - off[0];
-        if (deg == 0) continue;
-        if (deg == 1) { // only neighbour may be a self-loop (Graph500: degree >= 1 excluding self-loops)
-            uint32_t nb = 0;
-            BFSX_HIP_TRY(hipMemcpy(&nb, g->d_col + off[0], sizeof(nb), hipMemcpyDeviceToHost));
-            if ((int64_t)nb == x) continue;
+        int64_t ok = 0;
+        if (x >= g->v_lo && x < g->v_lo + g->nv) {
+            int64_t off[2];
+            BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + (x - g->v_lo), sizeof(off), hipMemcpyDeviceToHost));
+            const int64_t deg = off[1] - off[0];
+            ok = deg > 0;
+            if (deg == 1) { // only neighbour may be a self-loop (Graph500: degree >= 1 excluding self-loops)
+                uint32_t nb = 0;
+                BFSX_HIP_TRY(hipMemcpy(&nb, g->d_col + off[0], sizeof(nb), hipMemcpyDeviceToHost));
+                ok = (int64_t)nb != x;
+            }
         }
+        if (part) {
+            BFSX_HIP_TRY(hipMemcpyAsync(flag.p, &ok, sizeof(ok), hipMemcpyHostToDevice, st));
+            if (int e = cm->allreduce_sum(flag.p, 1, st)) return e;
+            BFSX_HIP_TRY(hipMemcpyAsync(&ok, flag.p, sizeof(ok), hipMemcpyDeviceToHost, st));
+            BFSX_HIP_TRY(hipStreamSynchronize(st));
+        }
+        if (!ok) continue;
         seen.insert(x);
         roots[found++] = x;
     }

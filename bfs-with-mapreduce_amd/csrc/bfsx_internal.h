@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -28,6 +29,18 @@ struct Options {
     int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
+};
+
+// ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------
+// Stream-ordered collectives on device buffers (RCCL, or an in-process group of host threads).
+struct Comm {
+    int rank = 0, nranks = 1;
+    virtual ~Comm() = default;
+    virtual int allreduce_sum(int64_t *d_buf, int n, hipStream_t st) = 0;              // in place
+    virtual int alltoall1(const int64_t *d_send, int64_t *d_recv, hipStream_t st) = 0; // one value per rank
+    virtual int alltoallv(const unsigned long long *d_send, const int64_t *scount, const int64_t *sdispl, unsigned long long *d_recv,
+                          const int64_t *rcount, const int64_t *rdispl, hipStream_t st) = 0; // host counts
+    virtual int allgather(const unsigned long long *d_in, int64_t n, unsigned long long *d_out, hipStream_t st) = 0;
 };
 
 // ---- kernels_build.hip -------------------------------------------------------------------
@@ -55,6 +68,8 @@ int dist_frontier_slice(bfsx_graph *g, unsigned long long *d_slice);
 int dist_bu_step(bfsx_graph *g, const unsigned long long *d_front_global);
 int dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local);
 int dist_finish(bfsx_graph *g);
+// the whole partitioned level loop with the exchanges through ctx->comm (collective over the ranks)
+int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 void bfs_workspace_free(BfsWorkspace *ws);
 
 } // namespace bfsx
@@ -64,6 +79,7 @@ struct bfsx_ctx {
     hipStream_t stream = nullptr;
     bfsx::Options opt;
     int num_cus = 256;
+    std::unique_ptr<bfsx::Comm> comm; // partitioned path: set by bfsx_comm_init / bfsx_comm_local_group
 };
 
 struct bfsx_graph {

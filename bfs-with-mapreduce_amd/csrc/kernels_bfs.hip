@@ -75,7 +75,10 @@ struct BfsWorkspace {
     // multi-GPU level state (bfsx_dist_*)
     u64 *remote = nullptr;              // unbucketed remote pairs
     int64_t remote_cap = 0;
-    u64 *d_dist_ctr = nullptr;          // [0] remote tail, [1..kMaxRanks] count, [...] cursor
+    u64 *d_dist_ctr = nullptr;          // kCtrWords: [0] remote tail, then count, cursor, recv count, sums
+    u64 *sendbuf = nullptr, *recvbuf = nullptr, *fglob = nullptr; // native exchange buffers
+    int64_t send_cap = 0, recv_cap = 0, fglob_words = 0;
+    int64_t nnz_global = -1;
     int d_level = 0, d_dir = BFSX_DIR_TOPDOWN;
     bool d_in_queue = true;
     int64_t d_nf = 0, d_mf = 0;
@@ -468,10 +471,16 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
 // pairs: per-workgroup destination histograms (LDS atomics), then one reservation atomic per
 // (workgroup, destination) and LDS-ranked scatter.
 constexpr int kMaxRanks = 64;
+// multi-GPU counter block: [0] remote tail | count[64] | cursor[64] | recv count[64] | level sums[16]
+constexpr int kCtrHead = 1 + 2 * kMaxRanks; // zeroed per top-down level
+constexpr int kCtrRecv = kCtrHead;
+constexpr int kCtrSums = kCtrHead + kMaxRanks;
+constexpr int kCtrWords = kCtrSums + 16;
 
-__global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, uint64_t n, uint32_t chunk,
-                                                      int nranks, u64 *__restrict__ dcount) {
+__global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
+                                                      uint32_t chunk, int nranks, u64 *__restrict__ dcount) {
     __shared__ uint32_t s_h[kMaxRanks];
+    const uint64_t n = *d_n;
     for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS)
@@ -481,11 +490,12 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pa
         if (s_h[d]) atomicAdd(&dcount[d], (u64)s_h[d]);
 }
 
-__global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, uint64_t n, uint32_t chunk,
-                                                        int nranks, const u64 *__restrict__ dcount,
+__global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
+                                                        uint32_t chunk, int nranks, const u64 *__restrict__ dcount,
                                                         u64 *__restrict__ dcursor, u64 *__restrict__ out) {
     __shared__ uint32_t s_h[kMaxRanks];
     __shared__ u64 s_base[kMaxRanks];
+    const uint64_t n = *d_n;
     for (uint64_t i0 = (uint64_t)blockIdx.x * kBS; i0 < n; i0 += (uint64_t)gridDim.x * kBS) {
         for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
         __syncthreads();
@@ -816,6 +826,28 @@ __global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, cons
     }
 }
 
+// Multi-GPU level close: one workgroup sums the level's counter shards into
+//   out[0..4] = local {n_f, m_f, m_u, scanned, rows/claims}   out[8..10] = copy of {n_f, m_f, m_u}
+// (the copy is all-reduced in place; the local half stays for the per-level record).
+__global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out) {
+    __shared__ u64 s[kStatFields][kShards];
+    for (int i = threadIdx.x; i < kShards; i += blockDim.x) {
+        s[0][i] = slot->sh[i].nf;
+        s[1][i] = slot->sh[i].mf;
+        s[2][i] = slot->sh[i].mu;
+        s[3][i] = slot->sh[i].scanned;
+        s[4][i] = slot->sh[i].claims;
+    }
+    __syncthreads();
+    if (threadIdx.x < kStatFields) {
+        u64 t = 0;
+        for (int i = 0; i < kShards; i++) t += s[threadIdx.x][i];
+        if (threadIdx.x == 0 && topdown) t = slot->qtail;
+        out[threadIdx.x] = (int64_t)t;
+        if (threadIdx.x < 3) out[8 + threadIdx.x] = (int64_t)t;
+    }
+}
+
 unsigned clamp_grid(int64_t blocks, unsigned cap) {
     if (blocks < 1) blocks = 1;
     return (unsigned)std::min<int64_t>(blocks, cap);
@@ -946,6 +978,7 @@ SlotSums sum_slot(const LevelSlot *s) {
 
 void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
+    for (void *p : {(void *)ws->sendbuf, (void *)ws->recvbuf, (void *)ws->fglob}) if (p) (void)hipFree(p);
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
                     (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
@@ -1154,7 +1187,7 @@ inline Part make_part(bfsx_graph *g, BfsWorkspace *ws) {
 int dist_ws(bfsx_graph *g) {
     int rc = ws_alloc(g);
     if (rc) return rc;
-    if (!g->ws->d_dist_ctr) BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, (1 + 2 * kMaxRanks) * sizeof(u64)));
+    if (!g->ws->d_dist_ctr) BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, kCtrWords * sizeof(u64)));
     return BFSX_OK;
 }
 
@@ -1238,7 +1271,7 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
         BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
     }
     if (send_cap < ws->d_mf) return fail(BFSX_E_ARG, "send buffer smaller than the local frontier's m_f");
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, (1 + 2 * kMaxRanks) * sizeof(u64), st));
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st));
     const Part pt = make_part(g, ws);
     if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, level, pt)) return e;
     u64 n_remote = 0;
@@ -1247,10 +1280,10 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
     u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
     if (n_remote > 0) {
         const unsigned gbk = clamp_grid(((int64_t)n_remote + kBS - 1) / kBS, 1024);
-        hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, (uint64_t)n_remote,
+        hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                            (uint32_t)g->chunk, P, dcount);
         BFSX_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, (uint64_t)n_remote,
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                            (uint32_t)g->chunk, P, dcount, dcursor, d_send);
         BFSX_HIP_TRY(hipGetLastError());
     }
@@ -1361,6 +1394,214 @@ int dist_finish(bfsx_graph *g) {
             g->level_stats[l].cum_ms = t;
             g->level_stats[l].kernel_ms = k;
         }
+    }
+    return BFSX_OK;
+}
+
+// ==== multi-GPU native level loop ===================================================================
+// The same level-synchronous loop as bfs_run, over a 1-D partition, with every exchange enqueued on
+// the BFS stream through ctx->comm (RCCL or the in-process group).  Host waits per level: one for a
+// bottom-up level (the all-reduced counters), two for a top-down level (+ the pair counts that size
+// the grouped send/recv).  Distances are level-synchronous, so they are bit-identical to bfs_run's.
+namespace {
+
+int grow(u64 *&buf, int64_t &cap, int64_t need) {
+    if (need <= cap) return BFSX_OK;
+    if (buf) BFSX_HIP_TRY(hipFree(buf));
+    buf = nullptr;
+    cap = std::max<int64_t>(need, cap + cap / 2);
+    BFSX_HIP_TRY(hipMalloc(&buf, cap * sizeof(u64)));
+    return BFSX_OK;
+}
+
+// level close: local sums + all-reduce of (n_f, m_f, m_u); returns [0..4] local, [8..10] global
+int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) {
+    hipStream_t st = g->ctx->stream;
+    const int level = ws->d_level;
+    int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
+    hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
+    if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3, st)) return e;
+    BFSX_HIP_TRY(hipMemcpyAsync(out, sums, 16 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    return BFSX_OK;
+}
+
+} // namespace
+
+int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
+    Comm *cm = g->ctx->comm.get();
+    if (!cm) return fail(BFSX_E_ARG, "no communicator on this context (bfsx_comm_init / bfsx_comm_local_group)");
+    if (cm->nranks != g->nranks || cm->rank != g->rank)
+        return fail(BFSX_E_ARG, "graph partition does not match the communicator's rank/size");
+    int rc = dist_ws(g);
+    if (rc) return rc;
+    BfsWorkspace *ws = g->ws;
+    hipStream_t st = g->ctx->stream;
+    const Options &opt = g->ctx->opt;
+    const int P = g->nranks;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    if (int e = grow(ws->fglob, ws->fglob_words, ws->nwords * P)) return e;
+    int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
+    int64_t h[16];
+    if (ws->nnz_global < 0) { // once per graph
+        h[0] = g->nnz;
+        BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, sizeof(int64_t), hipMemcpyHostToDevice, st));
+        if (int e = cm->allreduce_sum(sums + 8, 1, st)) return e;
+        BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        ws->nnz_global = h[0];
+    }
+    int64_t deg_local = 0;
+    if ((rc = dist_begin(g, source, &deg_local))) return rc;
+    h[0] = deg_local;
+    BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    if (int e = cm->allreduce_sum(sums + 8, 1, st)) return e;
+    BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    const int64_t deg = h[0];
+
+    int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
+    int64_t nf = 1, prev_nf = 0, mf = deg, mu = ws->nnz_global - deg, examined = 0;
+    int64_t visited_local = (source >= g->v_lo && source < g->v_lo + g->nv) ? 1 : 0;
+    int td_levels = 0, bu_levels = 0;
+    std::vector<int64_t> scount(P), sdispl(P), rcount(P), rdispl(P);
+    std::vector<u64> hc(2 * kMaxRanks);
+    for (;;) {
+        const int level = ws->d_level;
+        if (opt.direction == BFSX_DIR_AUTO && level > 0) {
+            if (dir == BFSX_DIR_TOPDOWN) {
+                if (mf > mu / std::max(opt.alpha, 1)) dir = BFSX_DIR_BOTTOMUP;
+            } else if (nf < g->nv_global / std::max(opt.beta, 1) && nf < prev_nf) {
+                dir = BFSX_DIR_TOPDOWN;
+            }
+        }
+        if (int e = dist_level_events(ws, level)) return e;
+        BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
+        const bool td = dir == BFSX_DIR_TOPDOWN;
+        if (td) {
+            if (!ws->d_in_queue) { // local bitmap slice -> queue
+                BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
+                const int64_t per_block_min = (int64_t)kBS * kCompactWords;
+                const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
+                const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
+                hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
+                                   ws->d_cursor);
+                BFSX_HIP_TRY(hipGetLastError());
+                ws->d_in_queue = true;
+            }
+            // remote pairs <= adjacency entries of the local frontier
+            const int64_t need = std::max<int64_t>(ws->d_mf, 1);
+            if (need > ws->remote_cap) {
+                if (ws->remote) BFSX_HIP_TRY(hipFree(ws->remote));
+                ws->remote = nullptr;
+                ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
+                BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
+            }
+            if (int e = grow(ws->sendbuf, ws->send_cap, need)) return e;
+            BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st));
+            const Part pt = make_part(g, ws);
+            if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, level, pt)) return e;
+            u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
+            // pair count read on the device: the grid is sized by its upper bound, the local m_f
+            const unsigned gbk = clamp_grid((need + kBS - 1) / kBS, 1024);
+            hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
+                               (uint32_t)g->chunk, P, dcount);
+            BFSX_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
+                               (uint32_t)g->chunk, P, dcount, dcursor, ws->sendbuf);
+            BFSX_HIP_TRY(hipGetLastError());
+            u64 *drecv = ws->d_dist_ctr + kCtrRecv;
+            if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
+                return e;
+            BFSX_HIP_TRY(hipMemcpyAsync(hc.data(), dcount, P * sizeof(u64), hipMemcpyDeviceToHost, st));
+            BFSX_HIP_TRY(hipMemcpyAsync(hc.data() + kMaxRanks, drecv, P * sizeof(u64), hipMemcpyDeviceToHost, st));
+            BFSX_HIP_TRY(hipStreamSynchronize(st));
+            int64_t so = 0, ro = 0;
+            for (int p = 0; p < P; p++) {
+                scount[p] = (int64_t)hc[p];
+                rcount[p] = (int64_t)hc[kMaxRanks + p];
+                sdispl[p] = so;
+                rdispl[p] = ro;
+                so += scount[p];
+                ro += rcount[p];
+            }
+            if (int e = grow(ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
+            if (int e = cm->alltoallv(ws->sendbuf, scount.data(), sdispl.data(), ws->recvbuf, rcount.data(),
+                                      rdispl.data(), st))
+                return e;
+            if (ro > 0) {
+                const dim3 grid(clamp_grid((ro + kBS - 1) / kBS, cap));
+                if (ws->off32)
+                    hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (uint32_t)ro,
+                                       ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo);
+                else
+                    hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (uint32_t)ro,
+                                       g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo);
+                BFSX_HIP_TRY(hipGetLastError());
+            }
+            td_levels++;
+        } else {
+            if (ws->d_in_queue) { // local queue -> bitmap slice
+                BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, ws->nwords * sizeof(u64), st));
+                hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0,
+                                   st, ws->qa, (uint32_t)ws->d_nf, ws->front);
+                BFSX_HIP_TRY(hipGetLastError());
+                ws->d_in_queue = false;
+            }
+            if (int e = cm->allgather(ws->front, ws->nwords, ws->fglob, st)) return e;
+            if (int e = launch_bu<true>(g, ws, ws->fglob, level)) return e;
+            bu_levels++;
+        }
+        if (int e = dist_level_close(g, ws, td, h)) return e;
+        // per-level record (local counts) and state advance
+        bfsx_level_stat ls{};
+        ls.direction = dir;
+        ls.level = level;
+        ls.frontier_in = ws->d_nf;
+        ls.frontier_out = h[0];
+        ls.mf_in = ws->d_mf;
+        ls.unvisited_in = g->nv - visited_local - ws->n_dead;
+        ls.scanned = h[3];
+        ls.claims = h[4];
+        g->level_stats.push_back(ls);
+        g->level_dirs.push_back(dir);
+        examined += h[3];
+        visited_local += h[0];
+        if (td) std::swap(ws->qa, ws->qb);
+        else std::swap(ws->front, ws->next);
+        ws->d_dir = dir;
+        ws->d_in_queue = td;
+        ws->d_nf = h[0];
+        ws->d_mf = h[1];
+        ws->d_level = level + 1;
+        prev_nf = nf;
+        nf = h[8];
+        mf = h[9];
+        mu = td ? mu - mf : h[10];
+        if (nf == 0) break;
+    }
+    if ((rc = dist_finish(g))) return rc;
+    if (stats) {
+        *stats = bfsx_stats{};
+        stats->levels = ws->d_level;
+        stats->topdown_levels = td_levels;
+        stats->bottomup_levels = bu_levels;
+        stats->edges_examined = examined;
+        float ms = 0.f;
+        BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
+        stats->t_bfs_ms = ms;
+        int64_t m = 0, r = 0;
+        if ((rc = bfs_mcomp(g, &m, &r))) return rc;
+        h[0] = m;
+        h[1] = r;
+        BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, 2 * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        if (int e = cm->allreduce_sum(sums + 8, 2, st)) return e;
+        BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        stats->m_comp = h[0];
+        stats->reached = h[1];
     }
     return BFSX_OK;
 }

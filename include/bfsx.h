@@ -122,7 +122,9 @@ int64_t bfsx_graph_m(const bfsx_graph *g);   /* input tuples */
 /* D2H copy of the CSR: row_off[nv+1], col[nnz] (either may be NULL).  Each row holds one
  * neighbour set; its order follows the "row_order" option the graph was built with. */
 int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col);
-/* Graph500 root sampling: count distinct vertices with a non-self-loop neighbour, seeded. */
+/* Graph500 root sampling: count distinct vertices with a non-self-loop neighbour, seeded.  On a
+ * partitioned graph it is collective over the context's communicator and returns, on every rank,
+ * the roots the single-device graph returns. */
 int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots);
 
 /* ---- the hot path ---------------------------------------------------------------------------- */
@@ -178,6 +180,22 @@ int bfsx_dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local);
 int bfsx_dist_finish(bfsx_graph *g);
 /* Local share of m_comp and of the reached count (the caller all-reduces them). */
 int bfsx_dist_mcomp(bfsx_graph *g, int64_t *m_local, int64_t *reached_local);
+
+/* ---- multi-GPU, native exchange: the whole partitioned level loop inside the library ------------
+ * One rank per GPU.  The exchange runs over RCCL (xGMI) on the BFS stream: top-down levels route
+ * (vertex, parent) pairs to their owners (all-to-all of counts + grouped send/recv), bottom-up levels
+ * all-gather the frontier bitmap slices, every level all-reduces (n_f, m_f, m_u).
+ * bfsx_comm_unique_id: rank 0 creates the RCCL id; the caller distributes the bytes (any channel).
+ * bfsx_comm_init: collective over the nranks processes; attaches the communicator to ctx.
+ * bfsx_comm_local_group: the same exchange for nranks contexts inside ONE process (one host thread
+ * per rank; ranks may share a device) -- the partitioned path testable on a single GPU.
+ * bfsx_dist_bfs: collective; every rank passes the same source.  Results: bfsx_result (local rows).
+ * stats, if requested, must be requested by every rank (m_comp/reached are all-reduced). */
+#define BFSX_COMM_ID_BYTES 128
+int bfsx_comm_unique_id(uint8_t *id);
+int bfsx_comm_init(bfsx_ctx *ctx, int rank, int nranks, const uint8_t *id);
+int bfsx_comm_local_group(bfsx_ctx **ctxs, int nranks);
+int bfsx_dist_bfs(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 
 /* ---- device synchronisation helper for benchmarking harnesses ------------------------------- */
 int bfsx_device_synchronize(bfsx_ctx *ctx);

@@ -1,0 +1,143 @@
+"""Partitioned BFS with the level loop AND the exchange inside libbfsx.so (bfsx_dist_bfs).
+
+The exchange layer has two implementations behind one interface (csrc/bfsx_comm.cpp): RCCL (one
+process per GPU, what bench.py --gpus N runs) and an in-process group (P ranks = P host threads of one
+process, device copies).  The box has one MI355X, so P = 2, 3, 4 run as an in-process group on device 0;
+the kernels, the owner routing, the bucketing, the count/pair exchanges, the all-gathered bottom-up
+frontier and the all-reduced direction switch are the code under test.  RCCL itself runs at P = 1
+(a communicator of one) in a fresh process.  Distances must be bit-exact against the oracle and the
+single-device path; parents are validated (Graph500 rules)."""
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+INF = 2147483647
+
+
+def run_group(bfsx, world, make_graph, sources, direction="auto", options=None):
+    """One thread per rank; returns per source: (stats, dist, parent, dirs) assembled globally."""
+    ctxs = [bfsx.Context(0, direction=direction, **(options or {})) for _ in range(world)]
+    graphs = [None] * world
+    try:
+        bfsx.local_group(ctxs)
+        for r in range(world):
+            graphs[r] = make_graph(ctxs[r], r, world)
+        out = []
+        for s in sources:
+            res, errs = [None] * world, []
+
+            def work(r):
+                try:
+                    st = graphs[r].dist_bfs(s)
+                    d, p = graphs[r].result()
+                    res[r] = (st, graphs[r].partition()["v_lo"], d, p, list(graphs[r].level_dirs()))
+                except Exception as e:  # noqa: BLE001 -- reported below
+                    errs.append(repr(e))
+
+            ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join(timeout=120)
+            assert not errs, errs
+            assert all(not t.is_alive() for t in ths), "rank thread hung"
+            nv = graphs[0].partition()["nv_global"]
+            dist = np.full(nv, INF, np.int32)
+            parent = np.full(nv, -1, np.int64)
+            for st, lo, d, p, _ in res:
+                dist[lo:lo + len(d)] = d
+                parent[lo:lo + len(p)] = p
+            keys = ("levels", "topdown_levels", "bottomup_levels", "m_comp", "reached")
+            assert all({k: r[0][k] for k in keys} == {k: res[0][0][k] for k in keys} for r in res), \
+                "ranks disagree on the all-reduced stats"
+            assert all(r[4] == res[0][4] for r in res), "ranks took different directions"
+            out.append((res[0][0], dist, parent, res[0][4]))
+        return out
+    finally:
+        for g in graphs:
+            if g is not None:
+                g.free()
+        for c in ctxs:
+            c.close()
+
+
+def check(nv, u, v, sources, out):
+    off, col = O.build_sets(nv, u, v)
+    for s, (st, dist, parent, _) in zip(sources, out):
+        ref, _ = O.csr_bfs(nv, off, col, s)
+        assert np.array_equal(dist, ref)
+        assert st["levels"] == int(ref[ref != INF].max()) + 1
+        assert O.validate(nv, off, col, s, dist, parent, rows_sorted=True) == 0
+        assert st["m_comp"] == O.mcomp(u, v, ref) and st["reached"] == int((ref != INF).sum())
+
+
+@pytest.mark.parametrize("world,direction", [(2, "auto"), (2, "topdown"), (2, "bottomup"), (3, "auto"),
+                                             (4, "auto"), (4, "bottomup")])
+def test_native_group_random(bfsx, world, direction):
+    rng = np.random.default_rng(100 + world)
+    nv = 6000
+    u = rng.integers(0, nv, 5 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 5 * nv).astype(np.uint32)
+    sources = [0, 2999, 5999]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, direction)
+    check(nv, u, v, sources, out)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_group_kronecker(bfsx, world):
+    scale, seed = 16, 0xD157
+    u, v = O.kronecker(scale, 16, seed)
+    nv = 1 << scale
+    sources = [int(u[0]), int(u[777])]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, seed=seed), sources)
+    check(nv, u, v, sources, out)
+    assert any(2 in o[3] for o in out)  # a bottom-up level ran against the all-gathered frontier
+    # the partitioned result equals the single-device result bit for bit
+    with bfsx.Context(0) as ctx, ctx.kronecker(scale, 16, seed) as g:
+        for s, o in zip(sources, out):
+            d, _, _ = g.bfs(s)
+            assert np.array_equal(d, o[1])
+
+
+@pytest.mark.parametrize("name", ["tinyCG", "mediumG", "tinyG"])
+def test_native_group_reference_files(bfsx, name):
+    nv, u, v = O.load_graphfileutil(os.path.join(GOLDEN, name + ".txt"))
+    world = 2
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), [0])
+    check(nv, u, v, [0], out)
+    ref = np.loadtxt(os.path.join(GOLDEN, name + ".dist"), dtype=np.int64)
+    ref = ref[:, 1] if ref.ndim == 2 else ref
+    assert np.array_equal(out[0][1].astype(np.int64), ref)
+
+
+def test_native_rccl_single_rank():
+    """RCCL communicator of one: the same loop over ncclAllGather / grouped send-recv / all-reduce."""
+    code = f"""
+import sys, os, numpy as np
+sys.path.insert(0, {os.path.join(ROOT, 'tests')!r})
+import conftest, oracle_py as O
+bfsx = conftest.load_bfsx()
+ctx = bfsx.Context(0)
+ctx.comm_init(0, 1, bfsx.comm_unique_id())
+u, v = O.kronecker(14, 16, 77)
+g = ctx.dist_kronecker(14, 0, 1, seed=77)
+ref_ctx = bfsx.Context(0)
+rg = ref_ctx.kronecker(14, 16, 77)
+for s in (int(u[0]), int(u[5])):
+    st = g.dist_bfs(s)
+    d, p = g.result()
+    d1, _, st1 = rg.bfs(s)
+    assert np.array_equal(d, d1), "rccl P=1 differs from the single-device path"
+    assert st["m_comp"] == st1["m_comp"] and st["levels"] == st1["levels"]
+print("rccl-ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "rccl-ok" in r.stdout, r.stdout + r.stderr
