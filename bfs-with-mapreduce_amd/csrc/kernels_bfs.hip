@@ -524,10 +524,10 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ 
 // ---- K5: bottom-up pull --------------------------------------------------------------------------
 // A wave owns 64 consecutive words of the visited bitmap (4096 vertices): one coalesced 512-B load
 // brings them into registers (lane k holds word w0+k).  The unvisited vertices of the group are
-// compacted lane-densely -- a wave prefix of per-word popcounts, a shuffle binary search for the
-// owning word and a popcount bit-select -- so every lane works on a live candidate whether the level
-// leaves half the vertices unvisited or one in a hundred.  Then two phases per round of kBuU*64
-// candidates:
+// compacted lane-densely -- a wave prefix of per-word popcounts gives every word its first rank, and
+// each round every word writes the ids of its unvisited bits ranked inside the round into an LDS
+// list -- so every lane works on a live candidate whether the level leaves half the vertices
+// unvisited or one in a hundred.  Then two phases per round of kBuU*64 candidates:
 //   A  every lane takes kBuU candidates at once: kBuU coalesced top1[v] loads (v's highest-degree
 //      neighbour), then kBuU independent frontier-bit probes -- the whole round costs two memory
 //      round trips instead of two per candidate.  Hits are done: no row offset is ever read for them.
@@ -565,6 +565,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
     __shared__ uint32_t s_miss[kWaves][kBuRound];
+    __shared__ uint32_t s_cand[kWaves][kBuRound];
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
     u64 acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0;
@@ -585,23 +586,27 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
         __builtin_amdgcn_wave_barrier();
         const uint32_t vbase = (uint32_t)(w0 * 64);
         for (uint32_t t0 = 0; t0 < total; t0 += kBuRound) {
+            // this round's candidates [t0, t0 + kBuRound) into LDS: each lane (one visited word) writes
+            // the ids of its unvisited bits whose wave-wide rank falls in the round
+            {
+                const uint32_t lo = excl > t0 ? excl : t0;
+                const uint32_t hi = min(excl + c, t0 + (uint32_t)kBuRound);
+                if (lo < hi) {
+                    u64 bits = unv;
+                    if (lo > excl) bits &= ~0ull << select_bit(unv, (int)(lo - excl));
+                    const uint32_t vb = vbase + lane * 64u;
+                    for (uint32_t idx = lo; idx < hi; idx++) {
+                        s_cand[wave][idx - t0] = vb + (uint32_t)(__ffsll((long long)bits) - 1);
+                        bits &= bits - 1ull;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
             uint32_t v[kBuU], x[kBuU];
             u64 fw[kBuU];
 #pragma unroll
-            for (int k = 0; k < kBuU; k++) {
-                // owning word (largest kk with excl[kk] <= idx) and bit, computed by every lane (shuffles
-                // need all lanes active); lanes past the end work on a clamped index and are masked
-                const uint32_t idx = t0 + (uint32_t)k * 64 + lane;
-                const uint32_t ic = idx < total ? idx : total - 1;
-                int kk = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1) {
-                    const uint32_t e = __shfl(excl, (kk + step) & 63);
-                    if (kk + step < 64 && e <= ic) kk += step;
-                }
-                const u64 uk = __shfl(unv, kk);
-                v[k] = vbase + (uint32_t)kk * 64 + (uint32_t)select_bit(uk, (int)(ic - __shfl(excl, kk)));
-            }
+            for (int k = 0; k < kBuU; k++) v[k] = s_cand[wave][k * 64 + lane]; // past `total`: masked below
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int k = 0; k < kBuU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < total) ? top1[v[k]] : 0u;
 #pragma unroll
@@ -1471,9 +1476,13 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     for (;;) {
         const int level = ws->d_level;
         if (opt.direction == BFSX_DIR_AUTO && level > 0) {
+            // Beamer's rule, plus the exchange cost: a top-down level ships up to 8*m_f*(P-1)/P bytes of
+            // (vertex, parent) pairs, a bottom-up level all-gathers an n/8-byte bitmap -- pull as soon as
+            // the pairs would outweigh the bitmap
+            const bool pairs_heavy = P > 1 && mf * 64 * (P - 1) > g->nv_global * P;
             if (dir == BFSX_DIR_TOPDOWN) {
-                if (mf > mu / std::max(opt.alpha, 1)) dir = BFSX_DIR_BOTTOMUP;
-            } else if (nf < g->nv_global / std::max(opt.beta, 1) && nf < prev_nf) {
+                if (mf > mu / std::max(opt.alpha, 1) || pairs_heavy) dir = BFSX_DIR_BOTTOMUP;
+            } else if (nf < g->nv_global / std::max(opt.beta, 1) && nf < prev_nf && !pairs_heavy) {
                 dir = BFSX_DIR_TOPDOWN;
             }
         }
