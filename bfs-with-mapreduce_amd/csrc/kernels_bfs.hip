@@ -542,20 +542,6 @@ constexpr int kBuU = 4;
 constexpr int kBuRound = 64 * kBuU;
 constexpr uint32_t kDeg1 = 0x80000000u;
 
-__device__ inline int select_bit(u64 x, int r) { // position of the r-th set bit (r < popc)
-    int pos = 0;
-#pragma unroll
-    for (int half = 32; half >= 1; half >>= 1) {
-        const int c = __popcll(x & ((1ull << half) - 1ull));
-        if (r >= c) {
-            r -= c;
-            x >>= half;
-            pos += half;
-        }
-    }
-    return pos;
-}
-
 template <class OffT, bool kMf>
 __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const u64 *__restrict__ front,
@@ -565,7 +551,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
     __shared__ uint32_t s_miss[kWaves][kBuRound];
-    __shared__ uint32_t s_cand[kWaves][kBuRound];
+    __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
     u64 acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0;
@@ -585,96 +571,98 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
         s_nx[wave][lane] = 0ull;
         __builtin_amdgcn_wave_barrier();
         const uint32_t vbase = (uint32_t)(w0 * 64);
-        for (uint32_t t0 = 0; t0 < total; t0 += kBuRound) {
-            // this round's candidates [t0, t0 + kBuRound) into LDS: each lane (one visited word) writes
-            // the ids of its unvisited bits whose wave-wide rank falls in the round
-            {
-                const uint32_t lo = excl > t0 ? excl : t0;
-                const uint32_t hi = min(excl + c, t0 + (uint32_t)kBuRound);
-                if (lo < hi) {
-                    u64 bits = unv;
-                    if (lo > excl) bits &= ~0ull << select_bit(unv, (int)(lo - excl));
-                    const uint32_t vb = vbase + lane * 64u;
-                    for (uint32_t idx = lo; idx < hi; idx++) {
-                        s_cand[wave][idx - t0] = vb + (uint32_t)(__ffsll((long long)bits) - 1);
-                        bits &= bits - 1ull;
+        // the group's candidates, one half (32 words, <= 2048 vertices) at a time: each word's lane
+        // writes the offsets of its unvisited bits at its rank, then rounds of kBuRound candidates
+        const uint32_t half = __shfl(incl, 31); // candidates in words 0..31
+        for (int h = 0; h < 2; h++) {
+            const uint32_t hb = h ? half : 0u, he = h ? total : half;
+            if (hb == he) continue; // wave-uniform
+            if ((lane >> 5) == (unsigned)h) {
+                u64 bits = unv;
+                uint32_t idx = excl - hb;
+                while (bits) {
+                    s_cand[wave][idx++] = (uint16_t)(lane * 64u + (uint32_t)(__ffsll((long long)bits) - 1));
+                    bits &= bits - 1ull;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t t0 = hb; t0 < he; t0 += kBuRound) {
+                uint32_t v[kBuU], x[kBuU];
+                u64 fw[kBuU];
+#pragma unroll
+                for (int k = 0; k < kBuU; k++) // past the half's end: masked below
+                    v[k] = vbase + s_cand[wave][t0 - hb + (uint32_t)k * 64 + lane];
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int k = 0; k < kBuU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < he) ? top1[v[k]] : 0u;
+#pragma unroll
+                for (int k = 0; k < kBuU; k++) {
+                    const uint32_t id = x[k] & ~fmask;
+                    fw[k] = (t0 + (uint32_t)k * 64 + lane < he) ? front[id >> 6] : 0ull;
+                }
+                uint32_t nmiss = 0; // wave-uniform
+#pragma unroll
+                for (int k = 0; k < kBuU; k++) {
+                    const bool ok = t0 + (uint32_t)k * 64 + lane < he;
+                    const uint32_t id = x[k] & ~fmask;
+                    const bool hit = ok && ((fw[k] >> (id & 63u)) & 1ull);
+                    const bool last = (x[k] & fmask) != 0; // top1 was the row's only entry
+                    if (ok) acc_sc += 1;
+                    if (hit) {
+                        stt[v[k]] = pack_state(id, nd);
+                        atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
+                        acc_nf += 1;
+                        if (kMf) acc_mf += (u64)(row_off[v[k] + 1] - row_off[v[k]]);
+                    } else if (ok && last) {
+                        acc_mu += 1;
                     }
+                    const bool miss = ok && !hit && !last;
+                    const u64 mm = __ballot(miss);
+                    if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
+                    nmiss += (uint32_t)__popcll(mm);
                 }
-            }
-            __builtin_amdgcn_wave_barrier();
-            uint32_t v[kBuU], x[kBuU];
-            u64 fw[kBuU];
-#pragma unroll
-            for (int k = 0; k < kBuU; k++) v[k] = s_cand[wave][k * 64 + lane]; // past `total`: masked below
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int k = 0; k < kBuU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < total) ? top1[v[k]] : 0u;
-#pragma unroll
-            for (int k = 0; k < kBuU; k++) {
-                const uint32_t id = x[k] & ~fmask;
-                fw[k] = (t0 + (uint32_t)k * 64 + lane < total) ? front[id >> 6] : 0ull;
-            }
-            uint32_t nmiss = 0; // wave-uniform
-#pragma unroll
-            for (int k = 0; k < kBuU; k++) {
-                const bool ok = t0 + (uint32_t)k * 64 + lane < total;
-                const uint32_t id = x[k] & ~fmask;
-                const bool hit = ok && ((fw[k] >> (id & 63u)) & 1ull);
-                const bool last = (x[k] & fmask) != 0; // top1 was the row's only entry
-                if (ok) acc_sc += 1;
-                if (hit) {
-                    stt[v[k]] = pack_state(id, nd);
-                    atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
-                    acc_nf += 1;
-                    if (kMf) acc_mf += (u64)(row_off[v[k] + 1] - row_off[v[k]]);
-                } else if (ok && last) {
-                    acc_mu += 1;
-                }
-                const bool miss = ok && !hit && !last;
-                const u64 mm = __ballot(miss);
-                if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
-                nmiss += (uint32_t)__popcll(mm);
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
-                if (m0 + lane < nmiss) {
-                    const uint32_t vv = s_miss[wave][m0 + lane];
-                    const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
-                    bool found = false;
-                    uint32_t par = 0;
-                    int64_t j = b + 1;
-                    while (!found && j < e) {
-                        const int64_t left = e - j;
-                        const uint32_t x0 = col[j];
-                        const uint32_t x1 = left > 1 ? col[j + 1] : x0;
-                        const uint32_t x2 = left > 2 ? col[j + 2] : x0;
-                        const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                        const bool h0 = (front[x0 >> 6] >> (x0 & 63u)) & 1ull;
-                        const bool h1 = (front[x1 >> 6] >> (x1 & 63u)) & 1ull;
-                        const bool h2 = (front[x2 >> 6] >> (x2 & 63u)) & 1ull;
-                        const bool h3 = (front[x3 >> 6] >> (x3 & 63u)) & 1ull;
-                        if (h0 | h1 | h2 | h3) {
-                            found = true;
-                            const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
-                            par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
-                            j += h + 1;
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
+                    if (m0 + lane < nmiss) {
+                        const uint32_t vv = s_miss[wave][m0 + lane];
+                        const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
+                        bool found = false;
+                        uint32_t par = 0;
+                        int64_t j = b + 1;
+                        while (!found && j < e) {
+                            const int64_t left = e - j;
+                            const uint32_t x0 = col[j];
+                            const uint32_t x1 = left > 1 ? col[j + 1] : x0;
+                            const uint32_t x2 = left > 2 ? col[j + 2] : x0;
+                            const uint32_t x3 = left > 3 ? col[j + 3] : x0;
+                            const bool h0 = (front[x0 >> 6] >> (x0 & 63u)) & 1ull;
+                            const bool h1 = (front[x1 >> 6] >> (x1 & 63u)) & 1ull;
+                            const bool h2 = (front[x2 >> 6] >> (x2 & 63u)) & 1ull;
+                            const bool h3 = (front[x3 >> 6] >> (x3 & 63u)) & 1ull;
+                            if (h0 | h1 | h2 | h3) {
+                                found = true;
+                                const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
+                                par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
+                                j += h + 1;
+                            } else {
+                                j += left < 4 ? left : 4;
+                            }
+                        }
+                        acc_sc += (u64)(j - b - 1);
+                        acc_rows += 1;
+                        if (found) {
+                            stt[vv] = pack_state(par, nd);
+                            atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
+                            acc_nf += 1;
+                            if (kMf) acc_mf += (u64)(e - b);
                         } else {
-                            j += left < 4 ? left : 4;
+                            acc_mu += (u64)(e - b);
                         }
                     }
-                    acc_sc += (u64)(j - b - 1);
-                    acc_rows += 1;
-                    if (found) {
-                        stt[vv] = pack_state(par, nd);
-                        atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
-                        acc_nf += 1;
-                        if (kMf) acc_mf += (u64)(e - b);
-                    } else {
-                        acc_mu += (u64)(e - b);
-                    }
                 }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_wave_barrier(); // the next half rewrites the list
         }
         const u64 nxl = s_nx[wave][lane];
         if (wl < nwords) {

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Counter exploration for one kernel (tuning aid): one rocprofv3 --pmc pass per counter group.
+#   usage (through gpurun): bash tools/pmc_explore.sh <tag> <kernel-regex>
+set -e -o pipefail
+TAG=$1; RE=$2
+OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline"
+i=0
+MODE=${3:-default}
+if [ "$MODE" = "sq" ]; then
+  set -- "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA" \
+         "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD"
+else
+  set -- "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum" \
+           "TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum" \
+           "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_UTCL2_BUSY GRBM_TA_BUSY" \
+           "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum TCC_TAG_STALL_sum"
+fi
+for grp in "$@"; do
+  i=$((i+1))
+  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "$RE" --output-format csv -d "$OUT/p$i" -o run -- $B \
+      > "$OUT/p$i.log" 2>&1
+done
+echo done > "$OUT/DONE"
