@@ -16,6 +16,7 @@
 // Row offsets are read as uint32 when the graph's adjacency has < 2^32 entries (half the bytes of the
 // int64 CSR offsets on every vertex probe), as int64 otherwise; every traversal kernel is templated on it.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <type_traits>
 
@@ -55,6 +56,12 @@ struct LevelSlot {
 };
 constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(u64));
 
+// A level's counter sums as the host reads them (mapped pinned memory, written by k_publish).
+struct alignas(64) Published {
+    u64 seq;
+    int64_t qtail, nf, mf, sc, cl, mu;
+};
+
 } // namespace
 
 struct BfsWorkspace {
@@ -69,6 +76,8 @@ struct BfsWorkspace {
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
     LevelSlot *ring = nullptr;          // device, 3 slots
     LevelSlot *h_slot = nullptr;        // pinned host mirror of one slot
+    Published *h_pub = nullptr, *d_pub = nullptr; // mapped pinned level counters (host / device view)
+    u64 pub_seq = 0;
     u64 *d_cursor = nullptr;            // bitmap -> queue compaction cursor
     u64 *d_red = nullptr;               // reductions (m_comp, reached)
     int64_t prev_source = -1;
@@ -133,21 +142,44 @@ __device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u
     }
 }
 
-// ---- K2: source init (after the visited bitmap is reset to the dead mask) -------------------------
+// ---- K2: BFS init: visited bitmap <- dead mask (+ the source bit), source state, counter slots ------
 // s: local row of the source (0xFFFFFFFF: the source is owned by another rank); sglob: its global id.
-__global__ void k_init_source(uint32_t s, uint32_t sglob, int64_t prev, const u64 *__restrict__ dead, u64 *stt,
-                              u64 *vis, uint32_t *q, LevelSlot *ring) {
+__global__ __launch_bounds__(kBS) void k_init(uint32_t s, uint32_t sglob, int64_t prev, const u64 *__restrict__ dead,
+                                              int64_t nwords, u64 *stt, u64 *__restrict__ vis, uint32_t *q,
+                                              LevelSlot *ring) {
+    const int64_t sw = s != 0xFFFFFFFFu ? (int64_t)(s >> 6) : -1;
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
+        vis[w] = dead[w] | (w == sw ? 1ull << (s & 63u) : 0ull);
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         // a previous isolated source is pre-visited (dead mask) so k_finalize never resets it
         if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) stt[prev] = kUnreached;
         if (s != 0xFFFFFFFFu) {
             stt[s] = pack_state(sglob, 0);
-            vis[s >> 6] |= 1ull << (s & 63u);
             q[0] = s;
         }
     }
     zero_slot(ring, -2); // slot 0
     zero_slot(ring, -1); // slot 1
+}
+
+// ---- level counters -> host: sums of the level's stat shards, published into mapped pinned host
+// memory with a sequence number the host spins on (a D2H copy + stream synchronise costs ~15 us per
+// level on MI355X, this ~9 us) ------------------------------------------------------------------
+__global__ void k_publish(const LevelSlot *__restrict__ slot, Published *pub, u64 seq) {
+    const unsigned lane = threadIdx.x; // one wave, lane i sums shard i
+    const StatShard &sh = slot->sh[lane];
+    const u64 nf = wave_sum(sh.nf), mf = wave_sum(sh.mf), sc = wave_sum(sh.scanned), cl = wave_sum(sh.claims),
+              mu = wave_sum(sh.mu);
+    if (lane == 0) {
+        pub->qtail = (int64_t)slot->qtail;
+        pub->nf = (int64_t)nf;
+        pub->mf = (int64_t)mf;
+        pub->sc = (int64_t)sc;
+        pub->cl = (int64_t)cl;
+        pub->mu = (int64_t)mu;
+        __threadfence_system();
+        *(volatile u64 *)&pub->seq = seq;
+    }
 }
 
 // ---- block-level output queue ------------------------------------------------------------------
@@ -867,6 +899,9 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipMalloc(&ws->top1, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->ring, 3 * sizeof(LevelSlot)));
     BFSX_HIP_TRY(hipHostMalloc(&ws->h_slot, sizeof(LevelSlot), hipHostMallocDefault));
+    BFSX_HIP_TRY(hipHostMalloc(&ws->h_pub, sizeof(Published), hipHostMallocMapped | hipHostMallocCoherent));
+    BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&ws->d_pub, ws->h_pub, 0));
+    ws->h_pub->seq = 0;
     BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(u64)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
@@ -955,6 +990,22 @@ struct SlotSums {
     int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0;
 };
 
+// Spin until k_publish of the current sequence number has landed; poll the stream now and then so a
+// faulted kernel surfaces as an error instead of a hang.
+int wait_published(BfsWorkspace *ws, hipStream_t st) {
+    const volatile u64 *seq = &ws->h_pub->seq;
+    for (uint64_t spin = 1; *seq != ws->pub_seq; spin++) {
+        if ((spin & 0xFFFF) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(BFSX_E_HIP, std::string("level kernels: ") + hipGetErrorString(e));
+            if (e == hipSuccess && *seq != ws->pub_seq) return fail(BFSX_E_HIP, "level counters were not published");
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return BFSX_OK;
+}
+
 SlotSums sum_slot(const LevelSlot *s) {
     SlotSums r;
     for (int i = 0; i < kShards; i++) {
@@ -978,6 +1029,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->d_dist_ctr})
         if (p) (void)hipFree(p);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
+    if (ws->h_pub) (void)hipHostFree(ws->h_pub);
     if (ws->ev_start) (void)hipEventDestroy(ws->ev_start);
     if (ws->ev_end) (void)hipEventDestroy(ws->ev_end);
     for (auto e : ws->ev_level) (void)hipEventDestroy(e);
@@ -1003,9 +1055,8 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
 
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
-    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, (uint32_t)source, (uint32_t)source, ws->prev_source,
-                       ws->dead, ws->st, ws->vis, ws->qa, ws->ring);
+    hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
+                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
     ws->prev_source = source;
 
@@ -1061,11 +1112,16 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             bu_levels++;
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-        BFSX_HIP_TRY(hipMemcpyAsync(ws->h_slot, ws->ring + (level + 1) % 3, sizeof(LevelSlot), hipMemcpyDeviceToHost,
-                                    st));
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
-        const SlotSums s = sum_slot(ws->h_slot);
-        const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? (int64_t)ws->h_slot->qtail : s.nf;
+        hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, ws->d_pub, ++ws->pub_seq);
+        BFSX_HIP_TRY(hipGetLastError());
+        if (int e = wait_published(ws, st)) return e;
+        SlotSums s;
+        s.nf = ws->h_pub->nf;
+        s.mf = ws->h_pub->mf;
+        s.sc = ws->h_pub->sc;
+        s.cl = ws->h_pub->cl;
+        s.mu = ws->h_pub->mu;
+        const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? ws->h_pub->qtail : s.nf;
         g->level_dirs.push_back(dir);
         bfsx_level_stat ls{};
         ls.direction = dir;
@@ -1212,9 +1268,10 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local) {
         deg = so[1] - so[0];
     }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
-    BFSX_HIP_TRY(hipMemcpyAsync(ws->vis, ws->dead, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_init_source, dim3(1), dim3(kBS), 0, st, owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)source,
-                       ws->prev_source, ws->dead, ws->st, ws->vis, ws->qa, ws->ring);
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    hipLaunchKernelGGL(k_init, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
+                       owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)source, ws->prev_source, ws->dead, ws->nwords,
+                       ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
     ws->prev_source = sl;
     ws->d_level = 0;
