@@ -713,6 +713,13 @@ __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restr
     }
 }
 
+// Frontier of a top-down level as a bitmap without one atomic per vertex: the visited bitmap after
+// the level XOR its snapshot from before the level (bits are only ever set).
+__global__ __launch_bounds__(kBS) void k_new_bits(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ snap) {
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
+        snap[w] ^= vis[w];
+}
+
 // Ballot/popcount compaction of a bitmap into a queue.  A workgroup owns a contiguous range of words
 // (kCompactWords per thread, coalesced), counts its set bits, scans the per-thread counts in LDS and
 // reserves its output range with ONE atomic; the grid is kept small (<= 256 workgroups) so the
@@ -1062,6 +1069,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     bool in_queue = true; // frontier currently held in ws->qa (else in ws->front)
+    bool snapped = false; // ws->front holds the visited bitmap from before the last (top-down) level
     int64_t nf = 1, prev_nf = 0;
     int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded (-1: unknown)
     int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
@@ -1088,9 +1096,14 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
         if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
-            BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
-            hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                               ws->qa, (uint32_t)nf, ws->front);
+            if (snapped) { // front holds the visited bitmap from before the last top-down level
+                hipLaunchKernelGGL(k_new_bits, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
+                                   ws->vis, nwords, ws->front);
+            } else {
+                BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
+                hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
+                                   ws->qa, (uint32_t)nf, ws->front);
+            }
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue) {
@@ -1103,7 +1116,14 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = true;
         }
+        snapped = false;
         if (dir == BFSX_DIR_TOPDOWN) {
+            // a wide top-down level may hand over to bottom-up: snapshot the visited bitmap (8 B per 64
+            // vertices) so its frontier bitmap is one XOR pass instead of one atomic per discovered vertex
+            if (mf >= nwords / 4 && opt.direction == BFSX_DIR_AUTO) {
+                BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
+                snapped = true;
+            }
             const Part pt{};
             if (int e = launch_td<false>(g, ws, nf, mf, level, pt)) return e;
             td_levels++;
