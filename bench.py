@@ -117,8 +117,12 @@ def measured_traffic(kernel="k_bu"):
             continue
         if rec.get("kernels_bfs_sha") == sha and kernel in rec.get("kernels", {}):
             k = rec["kernels"][kernel]
-            return {"traffic": round(k["traffic_B"] / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
-                    "traffic_source": os.path.relpath(path, ROOT), "fetch_correction": rec.get("fetch_correction")}
+            out = {"traffic": round(k["traffic_B"] / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
+                   "traffic_source": os.path.relpath(path, ROOT), "fetch_correction": rec.get("fetch_correction")}
+            if k.get("avg_ms_trace"):  # fabric-side rate of the same launches (rocprof trace durations)
+                out["traffic_GBs"] = round(k["traffic_B"] / (k["avg_ms_trace"] * 1e-3) / 1e9, 1)
+                out["traffic_frac"] = round(out["traffic_GBs"] / PEAK_HBM_GBS, 4)
+            return out
     return {"traffic": None, "traffic_source": "no PMC summary for this kernel source"}
 
 
