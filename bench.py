@@ -115,8 +115,9 @@ def measured_traffic(kernel="k_bu"):
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if rec.get("kernels_bfs_sha") == sha and kernel in rec.get("kernels", {}):
-            k = rec["kernels"][kernel]
+        names = [n for n in rec.get("kernels", {}) if n == kernel or n.startswith(kernel + "<")]
+        if rec.get("kernels_bfs_sha") == sha and names:
+            k = rec["kernels"][names[0]]
             out = {"traffic": round(k["traffic_B"] / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
                    "traffic_source": os.path.relpath(path, ROOT), "fetch_correction": rec.get("fetch_correction")}
             if k.get("avg_ms_trace"):  # fabric-side rate of the same launches (rocprof trace durations)
