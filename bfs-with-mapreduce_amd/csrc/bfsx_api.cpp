@@ -231,6 +231,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
     }
     if (k == "alpha") return as_int(ctx->opt.alpha);
     if (k == "beta") return as_int(ctx->opt.beta);
+    if (k == "offset_bits") {
+        if (v == "auto") ctx->opt.offset_bits = 0;
+        else if (v == "64") ctx->opt.offset_bits = 64;
+        else return fail(BFSX_E_ARG, "offset_bits must be auto|64");
+        return BFSX_OK;
+    }
     if (k == "hub_degree") {
         int h = 0;
         int rc = as_int(h);

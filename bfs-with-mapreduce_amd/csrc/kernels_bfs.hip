@@ -916,7 +916,8 @@ int ws_alloc(bfsx_graph *g) {
     const unsigned gfill = clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192);
     hipLaunchKernelGGL(k_fill64, dim3(gfill), dim3(kBS), 0, st, ws->st, (int64_t)nv, kUnreached);
     BFSX_HIP_TRY(hipGetLastError());
-    if (g->nnz < (int64_t)0xFFFFFFFFll) { // every offset (incl. row_off[nv] = nnz) fits in uint32
+    // every offset (incl. row_off[nv] = nnz) fits in uint32; "offset_bits=64" keeps the int64 path (tests)
+    if (g->nnz < (int64_t)0xFFFFFFFFll && g->ctx->opt.offset_bits != 64) {
         BFSX_HIP_TRY(hipMalloc(&ws->off32, (nv + 1) * sizeof(uint32_t)));
         hipLaunchKernelGGL(k_off32, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv + 1, ws->off32);
         BFSX_HIP_TRY(hipGetLastError());
@@ -1535,6 +1536,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     int64_t nf = 1, prev_nf = 0, mf = deg, mu = ws->nnz_global - deg, examined = 0;
     int64_t visited_local = (source >= g->v_lo && source < g->v_lo + g->nv) ? 1 : 0;
+    bool snapped = false; // ws->front holds the visited slice from before the last (top-down) level
     int td_levels = 0, bu_levels = 0;
     std::vector<int64_t> scount(P), sdispl(P), rcount(P), rdispl(P);
     std::vector<u64> hc(2 * kMaxRanks);
@@ -1554,6 +1556,8 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         if (int e = dist_level_events(ws, level)) return e;
         BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
         const bool td = dir == BFSX_DIR_TOPDOWN;
+        const bool was_snapped = snapped;
+        snapped = false;
         if (td) {
             if (!ws->d_in_queue) { // local bitmap slice -> queue
                 BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
@@ -1564,6 +1568,12 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                                    ws->d_cursor);
                 BFSX_HIP_TRY(hipGetLastError());
                 ws->d_in_queue = true;
+            }
+            // a wide top-down level may hand over to bottom-up: snapshot the visited slice (see bfs_run)
+            if (ws->d_mf >= ws->nwords / 4 && opt.direction == BFSX_DIR_AUTO) {
+                BFSX_HIP_TRY(
+                    hipMemcpyAsync(ws->front, ws->vis, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
+                snapped = true;
             }
             // remote pairs <= adjacency entries of the local frontier
             const int64_t need = std::max<int64_t>(ws->d_mf, 1);
@@ -1618,9 +1628,14 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             td_levels++;
         } else {
             if (ws->d_in_queue) { // local queue -> bitmap slice
-                BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, ws->nwords * sizeof(u64), st));
-                hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0,
-                                   st, ws->qa, (uint32_t)ws->d_nf, ws->front);
+                if (was_snapped) { // front holds the visited slice from before the last top-down level
+                    hipLaunchKernelGGL(k_new_bits, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0,
+                                       st, ws->vis, ws->nwords, ws->front);
+                } else {
+                    BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, ws->nwords * sizeof(u64), st));
+                    hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS),
+                                       0, st, ws->qa, (uint32_t)ws->d_nf, ws->front);
+                }
                 BFSX_HIP_TRY(hipGetLastError());
                 ws->d_in_queue = false;
             }

@@ -90,7 +90,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 30) ; "beta" = int (default 24)
  *   "hub_degree" = int (top-down multi-workgroup bin threshold, default 64)
  *   "row_order" = degree|id (adjacency order inside a CSR row for graphs built afterwards; default
- *                 degree = high-degree neighbours first, which shortens bottom-up probes) */
+ *                 degree = high-degree neighbours first, which shortens bottom-up probes)
+ *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
+ *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */

@@ -107,6 +107,17 @@ def test_native_group_kronecker(bfsx, world):
             assert np.array_equal(d, o[1])
 
 
+def test_native_group_int64_offsets(bfsx):
+    """The int64 row-offset kernels (graphs with >= 2^32 local adjacency entries) on the partitioned path."""
+    scale, seed = 14, 0xBEEF
+    u, v = O.kronecker(scale, 16, seed)
+    nv = 1 << scale
+    sources = [int(u[1]), int(v[2])]
+    out = run_group(bfsx, 3, lambda c, r, w: c.dist_kronecker(scale, r, w, seed=seed), sources,
+                    options={"offset_bits": "64"})
+    check(nv, u, v, sources, out)
+
+
 @pytest.mark.parametrize("name", ["tinyCG", "mediumG", "tinyG"])
 def test_native_group_reference_files(bfsx, name):
     nv, u, v = O.load_graphfileutil(os.path.join(GOLDEN, name + ".txt"))

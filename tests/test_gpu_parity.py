@@ -189,6 +189,26 @@ def test_row_order_option(ctx, order):
         ctx.set_option("row_order", "degree")
 
 
+@pytest.mark.parametrize("bits", ["auto", "64"])
+def test_offset_width_paths(ctx, bits):
+    """uint32 and int64 row-offset instantiations of every traversal kernel agree with the oracle (int64
+    is what graphs with >= 2^32 adjacency entries run; forced here on a small graph)."""
+    scale, seed = 14, 4242
+    ou, ov = O.kronecker(scale, 16, seed)
+    nv = 1 << scale
+    off, col = O.build_sets(nv, ou, ov)
+    ctx.set_option("offset_bits", bits)
+    try:
+        for direction in ("auto", "topdown", "bottomup"):
+            ctx.set_option("direction", direction)
+            with ctx.kronecker(scale, 16, seed) as g:
+                for r in g.sample_roots(3, seed=5):
+                    check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=False)
+    finally:
+        ctx.set_option("offset_bits", "auto")
+        ctx.set_option("direction", "auto")
+
+
 def test_kronecker_scale20_validated(ctx):
     """Full-size-style property check: Graph500 validation + oracle distances at scale 20."""
     scale = 20
