@@ -177,9 +177,14 @@ class DistBFS:
         levels = 0
         while True:
             if self.direction == "auto" and levels > 0:
-                if direction == "td" and mf > mu // self.alpha:
+                # Beamer's rule plus the exchange cost, as the native loop (kernels_bfs.hip
+                # dist_bfs_run): pull once a top-down level's pairs would outweigh the bitmap all-gather
+                world = self.c.world
+                pairs_heavy = world > 1 and mf * 64 * (world - 1) > self.nv_global * world
+                if direction == "td" and (mf > mu // self.alpha or pairs_heavy):
                     direction = "bu"
-                elif direction == "bu" and nf < self.nv_global // self.beta and nf < prev_nf:
+                elif (direction == "bu" and nf < self.nv_global // self.beta and nf < prev_nf
+                      and not pairs_heavy):
                     direction = "td"
             if direction == "td":
                 counts = e.td_expand()

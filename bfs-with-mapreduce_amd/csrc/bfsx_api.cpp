@@ -248,10 +248,9 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
 
 // rank/nranks > 1: 1-D partition -- this rank keeps the rows of global ids [rank*chunk, +chunk),
 // chunk = ceil(nv / nranks) rounded up to a multiple of 64 (frontier slices are whole bitmap words).
-static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m, int rank,
-                                   int nranks, bfsx_graph **out) {
+static bfsx_graph *new_partition(bfsx_ctx *ctx, int64_t nv, int64_t m, int rank, int nranks) {
     auto *g = new (std::nothrow) bfsx_graph();
-    if (!g) return fail(BFSX_E_OOM, "graph");
+    if (!g) return nullptr;
     g->ctx = ctx;
     g->m = m;
     g->nv_global = nv;
@@ -266,6 +265,13 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
         g->v_lo = 0;
         g->nv = nv;
     }
+    return g;
+}
+
+static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m, int rank,
+                                   int nranks, bfsx_graph **out) {
+    bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
+    if (!g) return fail(BFSX_E_OOM, "graph");
     int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, &g->d_row_off, &g->d_col,
                               &g->nnz, &g->d_tuple_cnt, g->v_lo, nv);
     if (rc) {
@@ -354,18 +360,18 @@ static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t se
     BFSX_HIP_TRY(hipSetDevice(ctx->device));
     const int64_t nv = (int64_t)1 << scale;
     const int64_t m = (int64_t)edgefactor << scale;
-    uint32_t *d_u = nullptr, *d_v = nullptr;
-    BFSX_HIP_TRY(hipMalloc(&d_u, m * sizeof(uint32_t)));
-    if (hipMalloc(&d_v, m * sizeof(uint32_t)) != hipSuccess) {
-        (void)hipFree(d_u);
-        return fail(BFSX_E_OOM, "device tuples");
-    }
-    int rc = kronecker_generate(ctx->stream, scale, edgefactor, seed, d_u, d_v);
-    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, rank, nranks, out);
+    // built straight from the counter stream: no tuple arrays (8 B per tuple, 137 GB at scale 30)
+    bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
+    if (!g) return fail(BFSX_E_OOM, "graph");
+    int rc = build_csr_kronecker(ctx->stream, scale, edgefactor, seed, ctx->opt.degree_order, &g->d_row_off,
+                                 &g->d_col, &g->nnz, &g->d_tuple_cnt, g->v_lo, g->nv);
     (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(d_u);
-    (void)hipFree(d_v);
-    return rc;
+    if (rc) {
+        delete g;
+        return rc;
+    }
+    *out = g;
+    return BFSX_OK;
 }
 
 int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, bfsx_graph **out) {

@@ -54,6 +54,10 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
                      uint32_t **d_tuple_cnt, int64_t lo = 0, int64_t nv_global = -1);
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v);
+// The same CSR built straight from the Kronecker counter stream (rows of global ids [lo, lo+nv_local)).
+int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order,
+                        int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, int64_t lo,
+                        int64_t nv_local);
 
 // ---- kernels_bfs.hip ---------------------------------------------------------------------
 struct BfsWorkspace;

@@ -10,7 +10,8 @@
 //   K1c scatter  per-row cursors (64-bit atomics) -> unsorted rows
 //   K1d sort     rocPRIM segmented radix sort of every row (chunked below 2^32 entries)
 //   K1e dedup    keep-flags (row head or != predecessor) -> scan -> compact -> new row offsets
-// The Kronecker generator (Graph500 recipe, counter-based RNG) also lives here.
+// The Kronecker generator (Graph500 recipe, counter-based RNG) also lives here; a Kronecker graph is
+// built straight from the counter stream (every pass regenerates its tuples, none are stored).
 #include <cstring>
 
 #include <rocprim/device/device_scan.hpp>
@@ -34,13 +35,96 @@ inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap = 16384) 
     return (unsigned)g;
 }
 
+// ---- Kronecker generator ---------------------------------------------------------------------
+__device__ __host__ inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+struct KronParams {
+    uint64_t sh;       // mix64(seed)
+    uint64_t mask;     // 2^scale - 1
+    uint64_t a1, c1, a2, c2;
+    int s1, s2, scale;
+    uint32_t t_ab, t_an, t_cn;
+};
+
+__device__ inline uint64_t kron_perm(uint64_t x, const KronParams &p) {
+    x = (x * p.a1 + p.c1) & p.mask;
+    x ^= x >> p.s1;
+    x = (x * p.a2 + p.c2) & p.mask;
+    x ^= x >> p.s2;
+    x = (x * p.a1 + p.c2) & p.mask;
+    return x;
+}
+
+// Tuple k of the stream: one counter-based draw per (k, bit), then the bijective relabel.
+__device__ inline void kron_tuple(const KronParams &p, int64_t k, uint32_t &u, uint32_t &v) {
+    uint64_t i = 0, j = 0;
+    for (int ib = 0; ib < p.scale; ib++) {
+        uint64_t r = mix64((((uint64_t)k) << 6 | (uint64_t)ib) ^ p.sh);
+        uint32_t r1 = (uint32_t)(r >> 32), r2 = (uint32_t)r;
+        uint64_t ii = r1 > p.t_ab;
+        uint64_t jj = r2 > (ii ? p.t_cn : p.t_an);
+        i |= ii << ib;
+        j |= jj << ib;
+    }
+    u = (uint32_t)kron_perm(i, p);
+    v = (uint32_t)kron_perm(j, p);
+}
+
+__global__ __launch_bounds__(kBS) void k_kronecker(KronParams p, int64_t m, uint32_t *__restrict__ u,
+                                                   uint32_t *__restrict__ v) {
+    for (int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x; k < m; k += (int64_t)gridDim.x * kBS)
+        kron_tuple(p, k, u[k], v[k]);
+}
+
+KronParams kron_params(int scale, uint64_t seed) {
+    KronParams p;
+    p.scale = scale;
+    p.sh = mix64(seed);
+    p.mask = (1ULL << scale) - 1;
+    p.a1 = (mix64(seed ^ 0xA5A5A5A5A5A5A5A5ULL) | 1ULL) & p.mask;
+    p.c1 = mix64(seed ^ 0x5A5A5A5A5A5A5A5AULL) & p.mask;
+    p.a2 = (mix64(seed ^ 0x3C3C3C3C3C3C3C3CULL) | 1ULL) & p.mask;
+    p.c2 = mix64(seed ^ 0xC3C3C3C3C3C3C3C3ULL) & p.mask;
+    p.s1 = scale / 2 + 1;
+    p.s2 = scale / 3 + 1;
+    // A,B,C,D = .57,.19,.19,.05: ab = .76, a_norm = 57/76, c_norm = 19/24, as 2^-32 fractions
+    p.t_ab = (uint32_t)((76ULL << 32) / 100ULL);
+    p.t_an = (uint32_t)((57ULL << 32) / 76ULL);
+    p.t_cn = (uint32_t)((19ULL << 32) / 24ULL);
+    return p;
+}
+
+// Tuple sources of the build: tuples held in device arrays (files, host tuples), or regenerated on
+// the fly from the Kronecker counter stream by every pass that needs them (no 8 B/tuple array: at
+// scale 30 that is 137 GB per device).
+struct ArraySrc {
+    const uint32_t *u, *v;
+    __device__ void operator()(int64_t i, uint32_t &a, uint32_t &b) const {
+        a = u[i];
+        b = v[i];
+    }
+};
+
+struct KronSrc {
+    KronParams p;
+    __device__ void operator()(int64_t i, uint32_t &a, uint32_t &b) const { kron_tuple(p, i, a, b); }
+};
+
+
 // Rows are built only for global ids in [lo, lo + nv) (the whole graph on one device); indices into
 // deg / tcnt / cursor are local (id - lo), adjacency entries stay global.
-__global__ __launch_bounds__(kBS) void k_count(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
-                                               int64_t m, uint32_t lo, uint32_t nv, uint32_t *__restrict__ deg,
+template <class Src>
+__global__ __launch_bounds__(kBS) void k_count(Src src, int64_t m, uint32_t lo, uint32_t nv, uint32_t *__restrict__ deg,
                                                uint32_t *__restrict__ tcnt) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
-        const uint32_t a = u[i] - lo, b = v[i] - lo; // unsigned wrap: out of range -> >= nv
+        uint32_t ua, vb;
+        src(i, ua, vb);
+        const uint32_t a = ua - lo, b = vb - lo; // unsigned wrap: out of range -> >= nv
         if (a < nv) {
             atomicAdd(&deg[a], 1u);
             atomicAdd(&tcnt[a], 1u);
@@ -49,11 +133,12 @@ __global__ __launch_bounds__(kBS) void k_count(const uint32_t *__restrict__ u, c
     }
 }
 
-__global__ __launch_bounds__(kBS) void k_scatter(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
-                                                 int64_t m, uint32_t lo, uint32_t nv,
+template <class Src>
+__global__ __launch_bounds__(kBS) void k_scatter(Src src, int64_t m, uint32_t lo, uint32_t nv,
                                                  unsigned long long *__restrict__ cursor, uint32_t *__restrict__ col) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
-        const uint32_t a = u[i], b = v[i];
+        uint32_t a, b;
+        src(i, a, b);
         if (a - lo < nv) col[atomicAdd(&cursor[a - lo], 1ull)] = b;
         if (b - lo < nv && a != b) col[atomicAdd(&cursor[b - lo], 1ull)] = a;
     }
@@ -61,10 +146,11 @@ __global__ __launch_bounds__(kBS) void k_scatter(const uint32_t *__restrict__ u,
 
 // Degree of every global id over the whole tuple list (duplicates counted): the row-order key of a
 // partitioned graph, whose neighbours' rows live on other ranks.
-__global__ __launch_bounds__(kBS) void k_count_all(const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
-                                                   int64_t m, uint32_t *__restrict__ deg) {
+template <class Src>
+__global__ __launch_bounds__(kBS) void k_count_all(Src src, int64_t m, uint32_t *__restrict__ deg) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBS) {
-        const uint32_t a = u[i], b = v[i];
+        uint32_t a, b;
+        src(i, a, b);
         atomicAdd(&deg[a], 1u);
         if (a != b) atomicAdd(&deg[b], 1u);
     }
@@ -108,48 +194,6 @@ struct U8ToI64 {
     __host__ __device__ int64_t operator()(uint8_t x) const { return (int64_t)x; }
 };
 
-// ---- Kronecker generator ---------------------------------------------------------------------
-__device__ __host__ inline uint64_t mix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ULL;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    return z ^ (z >> 31);
-}
-
-struct KronParams {
-    uint64_t sh;       // mix64(seed)
-    uint64_t mask;     // 2^scale - 1
-    uint64_t a1, c1, a2, c2;
-    int s1, s2, scale;
-    uint32_t t_ab, t_an, t_cn;
-};
-
-__device__ inline uint64_t kron_perm(uint64_t x, const KronParams &p) {
-    x = (x * p.a1 + p.c1) & p.mask;
-    x ^= x >> p.s1;
-    x = (x * p.a2 + p.c2) & p.mask;
-    x ^= x >> p.s2;
-    x = (x * p.a1 + p.c2) & p.mask;
-    return x;
-}
-
-__global__ __launch_bounds__(kBS) void k_kronecker(KronParams p, int64_t m, uint32_t *__restrict__ u,
-                                                   uint32_t *__restrict__ v) {
-    for (int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x; k < m; k += (int64_t)gridDim.x * kBS) {
-        uint64_t i = 0, j = 0;
-        for (int ib = 0; ib < p.scale; ib++) {
-            uint64_t r = mix64((((uint64_t)k) << 6 | (uint64_t)ib) ^ p.sh);
-            uint32_t r1 = (uint32_t)(r >> 32), r2 = (uint32_t)r;
-            uint64_t ii = r1 > p.t_ab;
-            uint64_t jj = r2 > (ii ? p.t_cn : p.t_an);
-            i |= ii << ib;
-            j |= jj << ib;
-        }
-        u[k] = (uint32_t)kron_perm(i, p);
-        v[k] = (uint32_t)kron_perm(j, p);
-    }
-}
-
 template <class T>
 struct DevBuf {
     T *p = nullptr;
@@ -172,20 +216,7 @@ struct DevBuf {
 
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v) {
-    KronParams p;
-    p.scale = scale;
-    p.sh = mix64(seed);
-    p.mask = (1ULL << scale) - 1;
-    p.a1 = (mix64(seed ^ 0xA5A5A5A5A5A5A5A5ULL) | 1ULL) & p.mask;
-    p.c1 = mix64(seed ^ 0x5A5A5A5A5A5A5A5AULL) & p.mask;
-    p.a2 = (mix64(seed ^ 0x3C3C3C3C3C3C3C3CULL) | 1ULL) & p.mask;
-    p.c2 = mix64(seed ^ 0xC3C3C3C3C3C3C3C3ULL) & p.mask;
-    p.s1 = scale / 2 + 1;
-    p.s2 = scale / 3 + 1;
-    // A,B,C,D = .57,.19,.19,.05: ab = .76, a_norm = 57/76, c_norm = 19/24, as 2^-32 fractions
-    p.t_ab = (uint32_t)((76ULL << 32) / 100ULL);
-    p.t_an = (uint32_t)((57ULL << 32) / 76ULL);
-    p.t_cn = (uint32_t)((19ULL << 32) / 24ULL);
+    const KronParams p = kron_params(scale, seed);
     int64_t m = (int64_t)edgefactor << scale;
     hipLaunchKernelGGL(k_kronecker, dim3(grid_for(m, kBS, 32768)), dim3(kBS), 0, stream, p, m, d_u, d_v);
     BFSX_HIP_TRY(hipGetLastError());
@@ -280,9 +311,11 @@ int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, i
     return BFSX_OK;
 }
 
-int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
-                     bool degree_order, int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out,
-                     uint32_t **d_tuple_cnt_out, int64_t lo, int64_t nv_global) {
+namespace {
+
+template <class Src>
+int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_order, int64_t **d_row_off_out,
+                   uint32_t **d_col_out, int64_t *nnz_out, uint32_t **d_tuple_cnt_out, int64_t lo, int64_t nv_global) {
     if (nv_global < 0) nv_global = nv;
     const bool partitioned = lo != 0 || nv != nv_global;
     DevBuf<uint32_t> deg, tcnt;
@@ -293,7 +326,7 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
     BFSX_HIP_TRY(hipMemsetAsync(deg.p, 0, (nv + 1) * sizeof(uint32_t), stream));
     BFSX_HIP_TRY(hipMemsetAsync(tcnt.p, 0, nv * sizeof(uint32_t), stream));
     if (m > 0) {
-        hipLaunchKernelGGL(k_count, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, (uint32_t)lo,
+        hipLaunchKernelGGL(k_count<Src>, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, src, m, (uint32_t)lo,
                            (uint32_t)nv, deg.p, tcnt.p);
         BFSX_HIP_TRY(hipGetLastError());
     }
@@ -320,7 +353,7 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
         BFSX_HIP_TRY(cursor.alloc(nv));
         BFSX_HIP_TRY(hipMemcpyAsync(cursor.p, off.p, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
         if (m > 0) {
-            hipLaunchKernelGGL(k_scatter, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, (uint32_t)lo,
+            hipLaunchKernelGGL(k_scatter<Src>, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, src, m, (uint32_t)lo,
                                (uint32_t)nv, (unsigned long long *)cursor.p, col.p);
             BFSX_HIP_TRY(hipGetLastError());
         }
@@ -385,7 +418,7 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
             BFSX_HIP_TRY(gdeg.alloc(nv_global));
             BFSX_HIP_TRY(hipMemsetAsync(gdeg.p, 0, nv_global * sizeof(uint32_t), stream));
             if (m > 0) {
-                hipLaunchKernelGGL(k_count_all, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, d_u, d_v, m, gdeg.p);
+                hipLaunchKernelGGL(k_count_all<Src>, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, src, m, gdeg.p);
                 BFSX_HIP_TRY(hipGetLastError());
             }
         }
@@ -398,6 +431,23 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
     *d_tuple_cnt_out = tcnt.release();
     *nnz_out = nnz;
     return BFSX_OK;
+}
+
+} // namespace
+
+int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
+                     bool degree_order, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt,
+                     int64_t lo, int64_t nv_global) {
+    return build_csr_impl(stream, nv, ArraySrc{d_u, d_v}, m, degree_order, d_row_off, d_col, nnz, d_tuple_cnt, lo,
+                          nv_global);
+}
+
+int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order,
+                        int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, int64_t lo,
+                        int64_t nv_local) {
+    const int64_t m = (int64_t)edgefactor << scale;
+    return build_csr_impl(stream, nv_local, KronSrc{kron_params(scale, seed)}, m, degree_order, d_row_off, d_col,
+                          nnz, d_tuple_cnt, lo, (int64_t)1 << scale);
 }
 
 } // namespace bfsx
