@@ -29,7 +29,7 @@ INF = 2147483647
 # Every symbol include/bfsx.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "bfsx_abi_version", "bfsx_last_error", "bfsx_init", "bfsx_finalize", "bfsx_set_option",
-    "bfsx_parse_algs4", "bfsx_free_host", "bfsx_graph_load_algs4", "bfsx_graph_from_edges",
+    "bfsx_parse_algs4", "bfsx_parse_algs4_gpu", "bfsx_free_host", "bfsx_graph_load_algs4", "bfsx_graph_from_edges",
     "bfsx_graph_kronecker", "bfsx_kronecker_edges", "bfsx_graph_free", "bfsx_graph_nv",
     "bfsx_graph_nnz", "bfsx_graph_m", "bfsx_graph_csr", "bfsx_sample_roots", "bfsx_bfs",
     "bfsx_result", "bfsx_level_times", "bfsx_level_dirs", "bfsx_level_stats",
@@ -84,6 +84,8 @@ def lib():
         L.bfsx_finalize.restype = None
         L.bfsx_set_option.argtypes = [_VP, C.c_char_p, C.c_char_p]
         L.bfsx_parse_algs4.argtypes = [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _U32PP, _U32PP]
+        L.bfsx_parse_algs4_gpu.argtypes = [_VP, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _U32PP,
+                                           _U32PP]
         L.bfsx_free_host.argtypes = [_VP]
         L.bfsx_free_host.restype = None
         L.bfsx_graph_load_algs4.argtypes = [_VP, C.c_char_p, C.POINTER(_VP)]
@@ -177,6 +179,21 @@ class Context:
 
     def set_option(self, key, value):
         _check(lib().bfsx_set_option(self._h, key.encode(), str(value).encode()))
+
+    def parse_algs4_gpu(self, path):
+        """The same parse with the edge lines tokenized on this device -> (nv, u, v)."""
+        nv, m = C.c_int64(), C.c_int64()
+        up, vp = C.POINTER(C.c_uint32)(), C.POINTER(C.c_uint32)()
+        _check(lib().bfsx_parse_algs4_gpu(self._h, os.fsencode(path), C.byref(nv), C.byref(m), C.byref(up),
+                                          C.byref(vp)))
+        try:
+            n = m.value
+            u = np.ctypeslib.as_array(up, shape=(max(n, 1),))[:n].copy()
+            v = np.ctypeslib.as_array(vp, shape=(max(n, 1),))[:n].copy()
+        finally:
+            lib().bfsx_free_host(up)
+            lib().bfsx_free_host(vp)
+        return nv.value, u, v
 
     def load_algs4(self, path):
         g = _VP()

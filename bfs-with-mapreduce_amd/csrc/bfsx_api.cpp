@@ -112,6 +112,46 @@ struct HostVec {
     }
 };
 
+// mmap a whole file (GraphFileUtil.java:46 new FileInputStream; IOException -> BFSX_E_IO)
+int map_file(const char *path, MappedFile &f) {
+    f.fd = open(path, O_RDONLY);
+    if (f.fd < 0) return fail(BFSX_E_IO, std::string("cannot open ") + path + ": " + strerror(errno));
+    struct stat sb;
+    if (fstat(f.fd, &sb) != 0) return fail(BFSX_E_IO, std::string("cannot stat ") + path);
+    f.n = (size_t)sb.st_size;
+    if (f.n) {
+        void *m = mmap(nullptr, f.n, PROT_READ, MAP_PRIVATE, f.fd, 0);
+        if (m == MAP_FAILED) return fail(BFSX_E_IO, std::string("cannot map ") + path);
+        f.p = (const char *)m;
+        madvise(m, f.n, MADV_SEQUENTIAL);
+    }
+    return BFSX_OK;
+}
+
+// The two header lines (GraphFileUtil.java:48,58-59): V with Integer.parseInt, the edge count read and
+// ignored.  Leaves the reader at the first edge line.
+int read_algs4_header(LineReader &lr, int64_t &nv) {
+    const char *ls;
+    size_t ll;
+    if (!lr.next(ls, ll)) return fail(BFSX_E_PARSE, "missing vertex count line (parseInt(null))");
+    int64_t V;
+    if (!parse_java_int(ls, ll, V)) return fail(BFSX_E_PARSE, "line 1: vertex count is not an int");
+    if (V < 0) return fail(BFSX_E_PARSE, "line 1: negative vertex count (HashMap capacity)");
+    nv = V > 0 ? V : 1; // vertex 0 is always created (GraphFileUtil.java:53)
+    lr.next(ls, ll);    // edge count, unused
+    return BFSX_OK;
+}
+
+// File -> device tuples with the GPU tokenizer (kernels_parse.hip).
+int load_algs4_device(bfsx_ctx *ctx, const char *path, int64_t &nv, int64_t &m, uint32_t *&d_u, uint32_t *&d_v) {
+    MappedFile f;
+    if (int rc = map_file(path, f)) return rc;
+    LineReader lr{f.p, f.n};
+    if (int rc = read_algs4_header(lr, nv)) return rc;
+    BFSX_HIP_TRY(hipSetDevice(ctx->device));
+    return parse_algs4_device(ctx->stream, f.p + lr.pos, f.n - lr.pos, nv, 3, &d_u, &d_v, &m);
+}
+
 } // namespace
 } // namespace bfsx
 
@@ -128,27 +168,12 @@ void bfsx_free_host(void *p) { free(p); }
 int bfsx_parse_algs4(const char *path, int64_t *nv_out, int64_t *m_out, uint32_t **u_out, uint32_t **v_out) {
     if (!path || !nv_out || !m_out || !u_out || !v_out) return fail(BFSX_E_ARG, "null argument");
     MappedFile f;
-    f.fd = open(path, O_RDONLY);
-    if (f.fd < 0) return fail(BFSX_E_IO, std::string("cannot open ") + path + ": " + strerror(errno));
-    struct stat sb;
-    if (fstat(f.fd, &sb) != 0) return fail(BFSX_E_IO, std::string("cannot stat ") + path);
-    f.n = (size_t)sb.st_size;
-    if (f.n) {
-        void *m = mmap(nullptr, f.n, PROT_READ, MAP_PRIVATE, f.fd, 0);
-        if (m == MAP_FAILED) return fail(BFSX_E_IO, std::string("cannot map ") + path);
-        f.p = (const char *)m;
-        madvise(m, f.n, MADV_SEQUENTIAL);
-    }
+    if (int rc = map_file(path, f)) return rc;
     LineReader lr{f.p, f.n};
     const char *ls;
     size_t ll;
-    // GraphFileUtil.java:48  int vertexCount = Integer.parseInt(reader.readLine());
-    if (!lr.next(ls, ll)) return fail(BFSX_E_PARSE, "missing vertex count line (parseInt(null))");
-    int64_t V;
-    if (!parse_java_int(ls, ll, V)) return fail(BFSX_E_PARSE, "line 1: vertex count is not an int");
-    if (V < 0) return fail(BFSX_E_PARSE, "line 1: negative vertex count (HashMap capacity)");
-    const int64_t nv = V > 0 ? V : 1; // vertex 0 is always created (GraphFileUtil.java:53)
-    lr.next(ls, ll);                  // GraphFileUtil.java:58-59: edge count, unused
+    int64_t nv = 0;
+    if (int rc = read_algs4_header(lr, nv)) return rc;
     HostVec<uint32_t> us, vs;
     int64_t lineno = 2;
     while (lr.next(ls, ll)) { // GraphFileUtil.java:60-66, to EOF
@@ -324,13 +349,43 @@ int bfsx_dist_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, con
 int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
     if (!ctx || !path || !out) return fail(BFSX_E_ARG, "null argument");
     int64_t nv = 0, m = 0;
-    uint32_t *u = nullptr, *v = nullptr;
-    int rc = bfsx_parse_algs4(path, &nv, &m, &u, &v);
+    uint32_t *d_u = nullptr, *d_v = nullptr;
+    int rc = load_algs4_device(ctx, path, nv, m, d_u, d_v);
     if (rc) return rc;
-    rc = bfsx_graph_from_edges(ctx, nv, u, v, m, out);
-    free(u);
-    free(v);
+    if (nv > (int64_t)INT32_MAX) rc = fail(BFSX_E_ARG, "nv must be < 2^31 on one device");
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, 0, 1, out);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
     return rc;
+}
+
+int bfsx_parse_algs4_gpu(bfsx_ctx *ctx, const char *path, int64_t *nv_out, int64_t *m_out, uint32_t **u_out,
+                         uint32_t **v_out) {
+    if (!ctx || !path || !nv_out || !m_out || !u_out || !v_out) return fail(BFSX_E_ARG, "null argument");
+    int64_t nv = 0, m = 0;
+    uint32_t *d_u = nullptr, *d_v = nullptr;
+    int rc = load_algs4_device(ctx, path, nv, m, d_u, d_v);
+    if (rc) return rc;
+    uint32_t *u = (uint32_t *)malloc(std::max<int64_t>(m, 1) * sizeof(uint32_t));
+    uint32_t *v = (uint32_t *)malloc(std::max<int64_t>(m, 1) * sizeof(uint32_t));
+    if (!u || !v) rc = fail(BFSX_E_OOM, "out of host memory");
+    if (!rc && m > 0 &&
+        (hipMemcpy(u, d_u, m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(v, d_v, m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = fail(BFSX_E_HIP, "D2H tuples");
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    if (rc) {
+        free(u);
+        free(v);
+        return rc;
+    }
+    *nv_out = nv;
+    *m_out = m;
+    *u_out = u;
+    *v_out = v;
+    return BFSX_OK;
 }
 
 int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, uint32_t *u, uint32_t *v) {

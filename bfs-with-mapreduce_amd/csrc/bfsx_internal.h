@@ -54,6 +54,11 @@ int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const 
                      uint32_t **d_tuple_cnt, int64_t lo = 0, int64_t nv_global = -1);
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v);
+// ---- kernels_parse.hip: GPU tokenizer of the algs4 edge lines (after the two header lines) -----
+// body/n: host bytes of the edge lines; first_lineno: file line number of the first of them.  On success
+// the tuples are device arrays of length *m (caller frees); errors match the host parser's.
+int parse_algs4_device(hipStream_t st, const char *body, size_t n, int64_t nv, int64_t first_lineno, uint32_t **d_u,
+                       uint32_t **d_v, int64_t *m);
 // The same CSR built straight from the Kronecker counter stream (rows of global ids [lo, lo+nv_local)).
 int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order,
                         int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, int64_t lo,

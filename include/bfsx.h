@@ -102,10 +102,14 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
  * library; release with bfsx_free_host. */
 int bfsx_parse_algs4(const char *path, int64_t *nv, int64_t *m, uint32_t **u, uint32_t **v);
 void bfsx_free_host(void *p);
+/* The same parse with the edge lines tokenized on the GPU (what bfsx_graph_load_algs4 uses; the tuples
+ * are copied back here only so the result can be compared): identical tuples, codes and line numbers. */
+int bfsx_parse_algs4_gpu(bfsx_ctx *ctx, const char *path, int64_t *nv, int64_t *m, uint32_t **u, uint32_t **v);
 
 /* ---- graph construction (device-resident CSR) ------------------------------------------------ */
 /* Replaces GraphFileUtil.convert (GraphFileUtil.java:45-69): parse + symmetrise + dedup into
- * neighbour sets, built as CSR on the GPU.  Self-loops are kept once (HashSet semantics). */
+ * neighbour sets, built as CSR on the GPU.  Self-loops are kept once (HashSet semantics).  The header
+ * lines are read on the host, the edge lines are tokenized on the GPU (kernels_parse.hip). */
 int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out);
 /* Same construction from an in-memory tuple list (host arrays of length m, ids < nv). */
 int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
