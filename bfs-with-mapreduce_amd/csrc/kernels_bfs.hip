@@ -42,7 +42,8 @@ struct alignas(64) StatShard {
     u64 scanned; // adjacency entries read (algorithmic-bytes accounting)
     u64 claims;  // top-down atomicOr claims attempted (diagnostics)
     u64 mu;      // bottom-up: degree sum of the candidates left unvisited (Beamer m_u, exact)
-    u64 pad[3];
+    u64 dmax;    // top-down: largest degree in the produced frontier (skips the hub bin when <= hub_deg)
+    u64 pad[2];
 };
 constexpr int kStatFields = 5;
 
@@ -59,7 +60,7 @@ constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(u64));
 // A level's counter sums as the host reads them (mapped pinned memory, written by k_publish).
 struct alignas(64) Published {
     u64 seq;
-    int64_t qtail, nf, mf, sc, cl, mu;
+    int64_t qtail, nf, mf, sc, cl, mu, dmax;
 };
 
 } // namespace
@@ -124,8 +125,20 @@ __device__ inline void zero_slot(LevelSlot *ring, int level) {
 
 // Block-uniform: reduce the per-thread stat values over the workgroup; threads 0..4 add them to this
 // workgroup's shard of the level's counters.  Order: nf, mf, scanned, claims, mu.
-__device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu) {
+__device__ inline u64 wave_max(u64 x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const u64 y = __shfl_xor(x, d);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+__device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu, u64 dmax = 0) {
     __shared__ u64 s_red[kStatFields][kWaves];
+    __shared__ u64 s_dmax[kWaves];
+    dmax = wave_max(dmax);
+    if (lane_id() == 0) s_dmax[threadIdx.x >> 6] = dmax;
     u64 v[kStatFields] = {nf, mf, scanned, claims, mu};
     const unsigned wave = threadIdx.x >> 6;
 #pragma unroll
@@ -139,6 +152,11 @@ __device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u
 #pragma unroll
         for (int w = 0; w < kWaves; w++) t += s_red[threadIdx.x][w];
         if (t) atomicAdd(reinterpret_cast<u64 *>(&slot->sh[blockIdx.x % kShards]) + threadIdx.x, t);
+    } else if (threadIdx.x == kStatFields) {
+        u64 t = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) t = s_dmax[w] > t ? s_dmax[w] : t;
+        if (t) atomicMax(&slot->sh[blockIdx.x % kShards].dmax, t);
     }
 }
 
@@ -169,7 +187,7 @@ __global__ void k_publish(const LevelSlot *__restrict__ slot, Published *pub, u6
     const unsigned lane = threadIdx.x; // one wave, lane i sums shard i
     const StatShard &sh = slot->sh[lane];
     const u64 nf = wave_sum(sh.nf), mf = wave_sum(sh.mf), sc = wave_sum(sh.scanned), cl = wave_sum(sh.claims),
-              mu = wave_sum(sh.mu);
+              mu = wave_sum(sh.mu), dmax = wave_max(sh.dmax);
     if (lane == 0) {
         pub->qtail = (int64_t)slot->qtail;
         pub->nf = (int64_t)nf;
@@ -177,6 +195,7 @@ __global__ void k_publish(const LevelSlot *__restrict__ slot, Published *pub, u6
         pub->sc = (int64_t)sc;
         pub->cl = (int64_t)cl;
         pub->mu = (int64_t)mu;
+        pub->dmax = (int64_t)dmax;
         __threadfence_system();
         *(volatile u64 *)&pub->seq = seq;
     }
@@ -293,7 +312,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
                                       int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn,
-                                      const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts) {
+                                      const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -325,7 +344,9 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
             if (valid[k] && !send && claim(vl, vis, attempts)) {
                 win = true;
                 stt[vl] = pack_state(pu[k], nd);
-                acc_mf += (u64)(row_off[vl + 1] - row_off[vl]);
+                const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
+                acc_mf += dg;
+                acc_dmax = dg > acc_dmax ? dg : acc_dmax;
             }
             bq_push(q, win, vl);
             if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
@@ -341,7 +362,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
                                             LevelSlot *ring, int level, uint32_t hub_deg,
-                                            uint32_t *__restrict__ hubs, Part pt) {
+                                            uint32_t *__restrict__ hubs, Part pt, int gsz) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
@@ -355,12 +376,14 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     if (kDist && threadIdx.x == 0) rq->n = 0;
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    u64 acc_mf = 0, attempts = 0, scanned = 0;
-    for (uint32_t base = blockIdx.x * kBS; base < qlen; base += gridDim.x * kBS) {
+    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0;
+    // gsz (<= kBS) frontier vertices per workgroup and step: a narrow frontier spreads over more
+    // workgroups, so each sweeps its rows in one step instead of several dependent ones
+    for (uint32_t base = blockIdx.x * gsz; base < qlen; base += gridDim.x * gsz) {
         const uint32_t i = base + tid;
         uint32_t deg = 0, u = 0;
         int64_t beg = 0;
-        if (i < qlen) {
+        if ((int)tid < gsz && i < qlen) {
             u = qin[i];
             beg = (int64_t)row_off[u];
             int64_t d = (int64_t)row_off[u + 1] - beg;
@@ -388,13 +411,13 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             scanned += total;
         }
         __syncthreads();
-        sweep_segments<kDist>(s_scan, s_beg, s_u, kBS, 0, total, row_off, col, vis, stt, nd, q, qout, cn, pt, rq,
-                              acc_mf, attempts);
+        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, nd, q, qout, cn, pt, rq,
+                              acc_mf, attempts, acc_dmax);
         __syncthreads();
     }
     bq_flush(q, qout, cn);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, scanned, attempts, 0);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax);
 }
 
 template <bool kDist, class OffT>
@@ -416,7 +439,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x;
     constexpr int kPer = kHubBatch / kBS;
-    u64 acc_mf = 0, attempts = 0, scanned = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0;
     __syncthreads();
     for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
         const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
@@ -458,12 +481,12 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
         sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, cn, pt,
-                              rq, acc_mf, attempts);
+                              rq, acc_mf, attempts, acc_dmax);
         __syncthreads();
     }
     bq_flush(q, qout, cn);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, scanned, attempts, 0);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax);
 }
 
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
@@ -477,7 +500,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     bq_init(q);
     __syncthreads();
     const int32_t nd = level + 1;
-    u64 acc_mf = 0, attempts = 0;
+    u64 acc_mf = 0, attempts = 0, acc_dmax = 0;
     for (uint32_t i0 = blockIdx.x * kBS; i0 < npairs; i0 += gridDim.x * kBS) {
         const uint32_t i = i0 + threadIdx.x;
         bool win = false;
@@ -488,7 +511,9 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
             if (claim(vl, vis, attempts)) {
                 win = true;
                 stt[vl] = pack_state((uint32_t)pr, nd);
-                acc_mf += (u64)(row_off[vl + 1] - row_off[vl]);
+                const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
+                acc_mf += dg;
+                acc_dmax = dg > acc_dmax ? dg : acc_dmax;
             }
         }
         bq_push(q, win, vl);
@@ -496,7 +521,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
         if (q.n > (uint32_t)(kQCap - kBS)) bq_flush(q, qout, cn);
     }
     bq_flush(q, qout, cn);
-    shard_add(cn, 0, acc_mf, 0, attempts, 0);
+    shard_add(cn, 0, acc_mf, 0, attempts, 0, acc_dmax);
 }
 
 // Multi-GPU: stable bucketing of remote pairs by owning rank (P <= kMaxRanks).  Two passes over the
@@ -940,18 +965,22 @@ int ws_alloc(bfsx_graph *g) {
 }
 
 // ---- launch helpers: one per traversal kernel, dispatching on the row-offset width -------------
+// dmax: largest degree in the frontier (< 0: unknown) -- the hub bin is skipped when no vertex exceeds
+// the hub degree
 template <bool kDist>
-int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int level, const Part &pt) {
+int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt) {
     hipStream_t st = g->ctx->stream;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     const uint32_t hub_deg = g->ctx->opt.hub_degree;
-    const dim3 grid(clamp_grid((nf + kBS - 1) / kBS, cap));
+    int gsz = 16;
+    while (gsz < kBS && (int64_t)gsz * 2 * g->ctx->num_cus < nf) gsz *= 2;
+    const dim3 grid(clamp_grid((nf + gsz - 1) / gsz, cap));
     // hubs: sized by the frontier's degree sum when known (mf < 0: after a bottom-up level)
-    const bool hubs = mf < 0 || mf > (int64_t)hub_deg;
+    const bool hubs = dmax >= 0 ? dmax > (int64_t)hub_deg : (mf < 0 || mf > (int64_t)hub_deg);
     const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt);
+                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
@@ -960,7 +989,7 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int level
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt);
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
@@ -1073,6 +1102,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     bool snapped = false; // ws->front holds the visited bitmap from before the last (top-down) level
     int64_t nf = 1, prev_nf = 0;
     int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded (-1: unknown)
+    int64_t dmax = mf;                    // its largest degree (-1: unknown)
     int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
@@ -1126,7 +1156,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 snapped = true;
             }
             const Part pt{};
-            if (int e = launch_td<false>(g, ws, nf, mf, level, pt)) return e;
+            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt)) return e;
             td_levels++;
         } else {
             if (int e = launch_bu<false>(g, ws, ws->front, level)) return e;
@@ -1161,10 +1191,12 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         if (dir == BFSX_DIR_TOPDOWN) {
             mu -= s.mf;
             mf = s.mf;
+            dmax = ws->h_pub->dmax;
             std::swap(ws->qa, ws->qb);
         } else {
             mu = s.mu; // exact: degree sum of the candidates this level left unvisited
             mf = -1;   // not accumulated by the single-GPU bottom-up step
+            dmax = -1;
             std::swap(ws->front, ws->next);
         }
         if (nf == 0) break;
@@ -1344,7 +1376,7 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
     if (send_cap < ws->d_mf) return fail(BFSX_E_ARG, "send buffer smaller than the local frontier's m_f");
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st));
     const Part pt = make_part(g, ws);
-    if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, level, pt)) return e;
+    if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, -1, level, pt)) return e;
     u64 n_remote = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&n_remote, ws->d_dist_ctr, sizeof(n_remote), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -1586,7 +1618,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             if (int e = grow(ws->sendbuf, ws->send_cap, need)) return e;
             BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st));
             const Part pt = make_part(g, ws);
-            if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, level, pt)) return e;
+            if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, -1, level, pt)) return e;
             u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
             const unsigned gbk = clamp_grid((need + kBS - 1) / kBS, 1024);
