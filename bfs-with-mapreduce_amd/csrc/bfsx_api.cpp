@@ -256,6 +256,19 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
     }
     if (k == "alpha") return as_int(ctx->opt.alpha);
     if (k == "beta") return as_int(ctx->opt.beta);
+    if (k == "persist") {
+        if (v == "on") ctx->opt.persist = true;
+        else if (v == "off") ctx->opt.persist = false;
+        else return fail(BFSX_E_ARG, "persist must be on|off");
+        return BFSX_OK;
+    }
+    if (k == "persist_blocks") {
+        if (v == "auto") {
+            ctx->opt.persist_blocks = 0;
+            return BFSX_OK;
+        }
+        return as_int(ctx->opt.persist_blocks);
+    }
     if (k == "offset_bits") {
         if (v == "auto") ctx->opt.offset_bits = 0;
         else if (v == "64") ctx->opt.offset_bits = 64;

@@ -28,6 +28,8 @@ struct Options {
     int alpha = 30;             // top-down -> bottom-up when m_f > m_u / alpha (tuned on scale 26)
     int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
+    bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
+    int persist_blocks = 0;     // K3p workgroups (0: one per CU)
     int offset_bits = 0;        // traversal row-offset width: 0 = uint32 when nnz < 2^32, else int64; 64 = int64
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
 };

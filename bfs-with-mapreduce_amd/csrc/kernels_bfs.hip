@@ -57,6 +57,14 @@ struct LevelSlot {
 };
 constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(u64));
 
+// K3p (persistent top-down, below): per-level records and the grid-barrier state of one launch.
+constexpr uint32_t kPersistNf = 8192; // widest frontier a K3p level may produce and still continue
+constexpr int kPersistLevels = 1024;  // levels per launch
+
+struct alignas(64) PersistRec {
+    u64 qtail, mf, dmax, scanned, claims, t_end, pad[2];
+};
+
 // A level's counter sums as the host reads them (mapped pinned memory, written by k_publish).
 struct alignas(64) Published {
     u64 seq;
@@ -78,6 +86,16 @@ struct BfsWorkspace {
     LevelSlot *ring = nullptr;          // device, 3 slots
     LevelSlot *h_slot = nullptr;        // pinned host mirror of one slot
     Published *h_pub = nullptr, *d_pub = nullptr; // mapped pinned level counters (host / device view)
+    // K3p (persistent top-down): output segments, workgroup records, barrier state (device) and the
+    // launch result (mapped pinned host memory)
+    uint32_t *persist_seg = nullptr;
+    u64 *persist_brec = nullptr;
+    void *persist_ctl = nullptr, *h_pout = nullptr, *d_pout = nullptr;
+    int persist_grid = 0;       // workgroups (<= one per CU, all co-resident)
+    size_t persist_lds = 0;     // dynamic LDS per workgroup (keeps one workgroup per CU)
+    u64 persist_bar = 0;        // barrier rounds completed on persist_ctl
+    bool persist_reset = true;  // persist_ctl must be zeroed before the next launch
+    double clock_khz = 100000.0; // device wall-clock rate
     u64 pub_seq = 0;
     u64 *d_cursor = nullptr;            // bitmap -> queue compaction cursor
     u64 *d_red = nullptr;               // reductions (m_comp, reached)
@@ -226,10 +244,10 @@ __device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
 }
 
 // Block-uniform: every thread calls after a __syncthreads().
-__device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn) {
+__device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, u64 *qtail) {
     const uint32_t n = q.n;
     if (n == 0) return;
-    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(&cn->qtail, (u64)n);
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(qtail, (u64)n);
     __syncthreads();
     const uint32_t gb = q.gbase;
     for (uint32_t i = threadIdx.x; i < n; i += kBS) qout[gb + i] = q.buf[i];
@@ -311,7 +329,7 @@ template <bool kDist, class OffT, class ScanT>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                      int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, LevelSlot *cn,
+                                      int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
@@ -352,7 +370,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
             if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
         }
         __syncthreads();
-        if (q.n > (uint32_t)(kQCap - kBS * kItems)) bq_flush(q, qout, cn);
+        if (q.n > (uint32_t)(kQCap - kBS * kItems)) bq_flush(q, qout, qtail);
         if (kDist && rq->n > (uint32_t)(kRCap - kBS * kItems)) rq_flush(*rq, pt);
     }
 }
@@ -411,11 +429,11 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             scanned += total;
         }
         __syncthreads();
-        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, nd, q, qout, cn, pt, rq,
+        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt, rq,
                               acc_mf, attempts, acc_dmax);
         __syncthreads();
     }
-    bq_flush(q, qout, cn);
+    bq_flush(q, qout, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax);
 }
@@ -480,13 +498,314 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
-        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, cn, pt,
+        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt,
                               rq, acc_mf, attempts, acc_dmax);
         __syncthreads();
     }
-    bq_flush(q, qout, cn);
+    bq_flush(q, qout, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax);
+}
+
+// ---- K3p: persistent top-down for narrow frontiers --------------------------------------------------
+// High-diameter graphs (largeG: >= 567 levels, BreadthFirstPaths.java:33) run hundreds of levels whose
+// frontiers hold a few thousand vertices: per level, two launches, the host round trip and a
+// chain of single-counter atomics cost more than the work.  One launch of at most one workgroup per
+// CU runs such levels back to back, with no same-address atomic on the level's critical path:
+//   * workgroup b takes the frontier slice [nf*b/G, nf*(b+1)/G) and sweeps its rows edge-parallel
+//     (as k_td); the vis word and the target's row offsets are loaded together, so a win costs no
+//     further round trip;
+//   * winners go straight to b's own output segment (kRegion slots; LDS counter, no global cursor),
+//     written through L2 (`sc1` stores), and b's level record {n, m_f, scanned, claims, d_max};
+//   * a grid barrier on 8 sharded arrival counters (one per `blockIdx % 8`); every workgroup then
+//     reads the G records (`sc1` loads), scans the counts into segment offsets and takes the same
+//     decision: continue, or stop when the BFS ends, the next frontier is no longer narrow (n_f >
+//     kPersistNf, or a slice could hold more than kRegion edges), Beamer's rule asks for bottom-up or
+//     the level budget is used up.  On stop every workgroup copies its segment into the contiguous
+//     queue the per-level kernels read.
+// Hand-off form (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table): every
+// handed-off byte (segment entries, records) is stored `sc1` and loaded `sc1`; every wave waits
+// vmcnt(0) before the workgroup barrier behind which one lane adds to the arrival counter; the poll
+// is an `sc1` load of every shard.  Visited words are claimed by device atomics (a stale plain
+// pre-check can only under-report a set bit), the state array is read only after the launch.
+constexpr uint32_t kRegion = 16384; // output slots per workgroup and level parity
+constexpr int kBarShards = 8;
+
+struct alignas(128) BarShard {
+    u64 v;
+    u64 pad[15];
+};
+struct alignas(128) PersistCtl {
+    BarShard arr[kBarShards]; // monotonic across launches (the host passes the rounds already done)
+    u64 abort;
+    u64 pad[7];
+};
+// host-visible result of one launch (mapped pinned memory, written by workgroup 0)
+struct alignas(64) PersistOut {
+    u64 levels, abort, t0, pad[5];
+    PersistRec rec[kPersistLevels];
+};
+
+__device__ inline void st_sc1(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_sc1(u64 *p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline uint32_t ld_sc1(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline u64 ld_sc1(const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Arrive on this workgroup's shard and wait until every shard holds `round` arrivals of each of its
+// workgroups.  Block-uniform; false: a workgroup raised abort (or this one timed out).
+__device__ inline bool grid_sync(PersistCtl *ctl, u64 round) {
+    __shared__ int s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const unsigned l = threadIdx.x, G = gridDim.x;
+        if (l == 0) __hip_atomic_fetch_add(&ctl->arr[blockIdx.x % kBarShards].v, 1ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        const u64 target = l < (unsigned)kBarShards ? round * (u64)((G - l + kBarShards - 1) / kBarShards) : 0ull;
+        int ok = 1;
+        for (uint32_t spin = 0;; spin++) {
+            const u64 x = l < (unsigned)kBarShards ? ld_sc1(&ctl->arr[l].v) : ~0ull;
+            if (__all(x >= target)) break;
+            if (ld_sc1(&ctl->abort)) {
+                ok = 0;
+                break;
+            }
+            if (spin > (1u << 22)) {
+                if (l == 0) st_sc1(&ctl->abort, 1ull);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (l == 0) s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+// alpha <= 0: no direction switch (direction forced top-down).  q0: the first level's frontier
+// (contiguous); seg: 2 parities x G segments of kRegion; brec: 2 parities x G records (4 words);
+// qfinal: the last frontier, contiguous.  bar0: barrier rounds completed by earlier launches.
+template <class OffT>
+__global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                                    const uint32_t *__restrict__ q0, uint32_t nf0, uint32_t *seg,
+                                                    u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
+                                                    u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
+                                                    int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
+                                                    PersistOut *out) {
+    extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
+    __shared__ uint32_t s_off[kBS + 1];
+    __shared__ uint32_t s_scan[kBS + 1];
+    __shared__ int64_t s_beg[kBS];
+    __shared__ uint32_t s_u[kBS];
+    __shared__ uint32_t s_wsum[kWaves];
+    __shared__ u64 s_red[4][kWaves];
+    __shared__ uint32_t s_n;
+    (void)s_dyn;
+    const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const unsigned G = gridDim.x, b = blockIdx.x;
+    if (b == 0) {
+        // the per-level kernels that follow expect clean counter slots (each zeroes two levels ahead)
+        u64 *p = reinterpret_cast<u64 *>(ring);
+        for (int i = tid; i < 3 * kSlotWords; i += kBS) p[i] = 0ull;
+        if (tid == 0) out->t0 = (u64)wall_clock64();
+    }
+    uint32_t nf = nf0;
+    int64_t mu = mu0;
+    for (int it = 0;; it++) {
+        const uint32_t *sin = seg + (size_t)((it + 1) & 1) * G * kRegion; // previous level's segments
+        uint32_t *sout = seg + (size_t)(it & 1) * G * kRegion + (size_t)b * kRegion;
+        u64 *rout = brec + (size_t)(it & 1) * G * 4;
+        const int32_t nd = level0 + it + 1;
+        if (tid == 0) s_n = 0;
+        u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0;
+        const uint32_t vb = (uint32_t)((u64)nf * b / G), ve = (uint32_t)((u64)nf * (b + 1) / G);
+        __syncthreads();
+        for (uint32_t base = vb; base < ve; base += kBS) {
+            const uint32_t i = base + tid;
+            const int n = (int)min((uint32_t)kBS, ve - base);
+            uint32_t deg = 0, u = 0;
+            int64_t beg = 0;
+            if (i < ve) {
+                if (it == 0) {
+                    u = q0[i];
+                } else { // segment s of frontier index i: the last with s_off[s] <= i
+                    int lo = 0, hi = (int)G - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (s_off[mid] <= i) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    u = ld_sc1(sin + (size_t)lo * kRegion + (i - s_off[lo]));
+                }
+                beg = (int64_t)row_off[u];
+                deg = (uint32_t)((int64_t)row_off[u + 1] - beg);
+            }
+            const uint32_t inc = wave_incl_scan(deg);
+            if (lane == 63) s_wsum[wave] = inc;
+            __syncthreads();
+            uint32_t woff = 0, total = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t t = s_wsum[w];
+                woff += (w < (int)wave) ? t : 0u;
+                total += t;
+            }
+            s_scan[tid] = woff + inc - deg;
+            s_beg[tid] = beg;
+            s_u[tid] = u;
+            if (tid == 0) scanned += total;
+            __syncthreads();
+            for (uint32_t x0 = 0; x0 < total; x0 += kBS * kItems) {
+                uint32_t v[kItems], pu[kItems];
+                bool valid[kItems];
+#pragma unroll
+                for (int k = 0; k < kItems; k++) {
+                    const uint32_t x = x0 + (uint32_t)k * kBS + tid;
+                    valid[k] = x < total;
+                    v[k] = 0;
+                    pu[k] = 0;
+                    if (valid[k]) {
+                        int lo = 0, hi = n - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (s_scan[mid] <= x) lo = mid;
+                            else hi = mid - 1;
+                        }
+                        v[k] = col[s_beg[lo] + (int64_t)(x - s_scan[lo])];
+                        pu[k] = s_u[lo];
+                    }
+                }
+                // the visited word and the target's row bounds in one round trip
+                u64 wv[kItems];
+                int64_t r0[kItems], r1[kItems];
+#pragma unroll
+                for (int k = 0; k < kItems; k++) {
+                    wv[k] = valid[k] ? vis[v[k] >> 6] : ~0ull;
+                    r0[k] = valid[k] ? (int64_t)row_off[v[k]] : 0;
+                    r1[k] = valid[k] ? (int64_t)row_off[v[k] + 1] : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < kItems; k++) {
+                    const u64 bit = 1ull << (v[k] & 63u);
+                    bool win = false;
+                    if (!(wv[k] & bit)) {
+                        attempts++;
+                        win = !(atomicOr(vis + (v[k] >> 6), bit) & bit);
+                    }
+                    if (win) {
+                        stt[v[k]] = pack_state(pu[k], nd);
+                        const u64 dg = (u64)(r1[k] - r0[k]);
+                        acc_mf += dg;
+                        acc_dmax = dg > acc_dmax ? dg : acc_dmax;
+                    }
+                    const u64 mask = __ballot(win);
+                    if (mask) {
+                        const int leader = __ffsll((long long)mask) - 1;
+                        uint32_t pos = 0;
+                        if ((int)lane == leader) pos = atomicAdd(&s_n, (uint32_t)__popcll(mask));
+                        pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                        if (win) {
+                            if (pos < kRegion) st_sc1(sout + pos, v[k]);
+                            else st_sc1(&ctl->abort, 1ull); // cannot happen: slices are bounded on entry
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // this workgroup's level record
+        {
+            const u64 v0 = wave_sum(acc_mf), v1 = wave_sum(scanned), v2 = wave_sum(attempts), v3 = wave_max(acc_dmax);
+            if (lane == 0) {
+                s_red[0][wave] = v0;
+                s_red[1][wave] = v1;
+                s_red[2][wave] = v2;
+                s_red[3][wave] = v3;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                u64 a = 0, c = 0, d = 0, m = 0;
+                for (int w = 0; w < kWaves; w++) {
+                    a += s_red[0][w];
+                    c += s_red[1][w];
+                    d += s_red[2][w];
+                    m = s_red[3][w] > m ? s_red[3][w] : m;
+                }
+                st_sc1(rout + 4 * b + 0, (u64)s_n | (m << 32));
+                st_sc1(rout + 4 * b + 1, a);
+                st_sc1(rout + 4 * b + 2, c);
+                st_sc1(rout + 4 * b + 3, d);
+            }
+        }
+        if (!grid_sync(ctl, bar0 + (u64)it + 1)) {
+            if (b == 0 && tid == 0) {
+                out->abort = 1;
+                out->levels = (u64)it;
+            }
+            return;
+        }
+        // every workgroup: the G records -> segment offsets and the level's sums
+        u64 r_n = 0, r_dm = 0, r_mf = 0, r_sc = 0, r_cl = 0;
+        if (tid < G) {
+            const u64 w0 = ld_sc1(rout + 4 * tid);
+            r_n = w0 & 0xFFFFFFFFull;
+            r_dm = w0 >> 32;
+            r_mf = ld_sc1(rout + 4 * tid + 1);
+            r_sc = ld_sc1(rout + 4 * tid + 2);
+            r_cl = ld_sc1(rout + 4 * tid + 3);
+        }
+        const uint32_t inc = wave_incl_scan((uint32_t)r_n);
+        const u64 smf = wave_sum(r_mf), ssc = wave_sum(r_sc), scl = wave_sum(r_cl), sdm = wave_max(r_dm);
+        __syncthreads(); // s_red / s_wsum reuse
+        if (lane == 63) s_wsum[wave] = inc;
+        if (lane == 0) {
+            s_red[0][wave] = smf;
+            s_red[1][wave] = ssc;
+            s_red[2][wave] = scl;
+            s_red[3][wave] = sdm;
+        }
+        __syncthreads();
+        uint32_t woff = 0, nf_new = 0;
+        u64 mf_new = 0, sc_new = 0, cl_new = 0, dm_new = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) {
+            woff += (w < (int)wave) ? s_wsum[w] : 0u;
+            nf_new += s_wsum[w];
+            mf_new += s_red[0][w];
+            sc_new += s_red[1][w];
+            cl_new += s_red[2][w];
+            dm_new = s_red[3][w] > dm_new ? s_red[3][w] : dm_new;
+        }
+        const uint32_t my_n = (uint32_t)r_n;
+        s_off[tid] = woff + inc - my_n; // entries past G: unused
+        if (tid == 0) s_off[kBS] = nf_new;
+        if (b == 0 && tid == 0) {
+            PersistRec &r = out->rec[it];
+            r.qtail = nf_new;
+            r.mf = mf_new;
+            r.dmax = dm_new;
+            r.scanned = sc_new;
+            r.claims = cl_new;
+            r.t_end = (u64)wall_clock64();
+            out->levels = (u64)(it + 1);
+        }
+        mu -= (int64_t)mf_new;
+        const bool stop = nf_new == 0 || nf_new > kPersistNf ||
+                          (u64)((nf_new + G - 1) / G) * dm_new > (u64)kRegion ||
+                          (alpha > 0 && (int64_t)mf_new > mu / alpha) || it + 1 >= max_levels;
+        __syncthreads();
+        if (stop) { // hand the frontier back contiguous
+            const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
+            for (uint32_t i = tid; i < nb; i += kBS) qfinal[ob + i] = ld_sc1(sout + i);
+            return;
+        }
+        nf = nf_new;
+    }
 }
 
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
@@ -518,9 +837,9 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
         }
         bq_push(q, win, vl);
         __syncthreads();
-        if (q.n > (uint32_t)(kQCap - kBS)) bq_flush(q, qout, cn);
+        if (q.n > (uint32_t)(kQCap - kBS)) bq_flush(q, qout, &cn->qtail);
     }
-    bq_flush(q, qout, cn);
+    bq_flush(q, qout, &cn->qtail);
     shard_add(cn, 0, acc_mf, 0, attempts, 0, acc_dmax);
 }
 
@@ -1055,11 +1374,102 @@ SlotSums sum_slot(const LevelSlot *s) {
     return r;
 }
 
+struct LevelTiming {
+    int ev;        // event slot: this level's own (per-level kernels) or the K3p launch's begin event
+    bool persisted;
+    double rel_ms; // K3p: end of the level after the launch's start (device wall clock)
+    double k_ms;   // K3p: the level's own span
+};
+
+// K3p geometry: at most one workgroup per CU and at most kBS (every workgroup reads all records).
+int persist_blocks(const bfsx_ctx *ctx) {
+    const int want = ctx->opt.persist_blocks > 0 ? ctx->opt.persist_blocks : ctx->num_cus;
+    return std::max(1, std::min({want, ctx->num_cus, kBS}));
+}
+
+// Whether a top-down level of nf vertices (largest degree dmax, < 0: unknown) may start K3p: every
+// workgroup's slice must fit its output segment whatever it discovers.
+bool persist_fits(const bfsx_ctx *ctx, int64_t nf, int64_t dmax) {
+    if (!ctx->opt.persist || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
+    const int64_t G = persist_blocks(ctx);
+    return ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
+}
+
+// Run K3p from `level` (frontier of nf vertices in ws->qa; its last frontier lands in ws->qb).
+// Returns the number of levels it ran (>= 1) with their records in the PersistOut, or an error.
+int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu) {
+    hipStream_t st = g->ctx->stream;
+    const Options &opt = g->ctx->opt;
+    if (!ws->persist_seg) {
+        const int G = persist_blocks(g->ctx);
+        ws->persist_grid = G;
+        BFSX_HIP_TRY(hipMalloc(&ws->persist_seg, (size_t)2 * G * kRegion * sizeof(uint32_t)));
+        BFSX_HIP_TRY(hipMalloc(&ws->persist_brec, (size_t)2 * G * 4 * sizeof(u64)));
+        BFSX_HIP_TRY(hipMalloc(&ws->persist_ctl, sizeof(PersistCtl)));
+        BFSX_HIP_TRY(hipHostMalloc(&ws->h_pout, sizeof(PersistOut), hipHostMallocMapped | hipHostMallocCoherent));
+        BFSX_HIP_TRY(hipHostGetDevicePointer(&ws->d_pout, ws->h_pout, 0));
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, g->ctx->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        ws->clock_khz = (double)khz;
+        // more than half a CU's LDS per workgroup: the dispatcher can place only one per CU
+        int lds_cu = 0;
+        hipFuncAttributes fa{};
+        const void *kfn = ws->off32 ? reinterpret_cast<const void *>(&k_td_persist<uint32_t>)
+                                    : reinterpret_cast<const void *>(&k_td_persist<int64_t>);
+        if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, g->ctx->device) ==
+                hipSuccess &&
+            hipFuncGetAttributes(&fa, kfn) == hipSuccess && lds_cu > 0) {
+            const size_t want = (size_t)lds_cu / 2 + 1024;
+            const size_t dyn = want > fa.sharedSizeBytes ? want - fa.sharedSizeBytes : 0;
+            if (dyn && hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) == hipSuccess)
+                ws->persist_lds = dyn;
+            (void)hipGetLastError();
+        }
+    }
+    if (ws->persist_reset) {
+        BFSX_HIP_TRY(hipMemsetAsync(ws->persist_ctl, 0, sizeof(PersistCtl), st));
+        ws->persist_bar = 0;
+        ws->persist_reset = false;
+    }
+    auto *out = reinterpret_cast<PersistOut *>(ws->h_pout);
+    out->levels = 0;
+    out->abort = 0;
+    const int alpha = opt.direction == BFSX_DIR_AUTO ? std::max(opt.alpha, 1) : 0;
+    auto *ctl = reinterpret_cast<PersistCtl *>(ws->persist_ctl);
+    auto *dout = reinterpret_cast<PersistOut *>(ws->d_pout);
+    const dim3 grid(ws->persist_grid);
+    if (ws->off32)
+        hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
+                           (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
+                           mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout);
+    else
+        hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
+                           (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
+                           mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (out->abort) {
+        ws->persist_reset = true;
+        return fail(BFSX_E_HIP, "persistent top-down: grid barrier timed out or a segment overflowed");
+    }
+    if (out->levels < 1 || out->levels > (u64)kPersistLevels) {
+        ws->persist_reset = true;
+        return fail(BFSX_E_HIP, "persistent top-down: no level ran");
+    }
+    ws->persist_bar += out->levels;
+    return (int)out->levels;
+}
+
 } // namespace
 
 void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
-    for (void *p : {(void *)ws->sendbuf, (void *)ws->recvbuf, (void *)ws->fglob}) if (p) (void)hipFree(p);
+    for (void *p : {(void *)ws->sendbuf, (void *)ws->recvbuf, (void *)ws->fglob, (void *)ws->persist_seg,
+                    (void *)ws->persist_brec, ws->persist_ctl})
+        if (p) (void)hipFree(p);
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
                     (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
@@ -1067,6 +1477,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
         if (p) (void)hipFree(p);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->h_pub) (void)hipHostFree(ws->h_pub);
+    if (ws->h_pout) (void)hipHostFree(ws->h_pout);
     if (ws->ev_start) (void)hipEventDestroy(ws->ev_start);
     if (ws->ev_end) (void)hipEventDestroy(ws->ev_end);
     for (auto e : ws->ev_level) (void)hipEventDestroy(e);
@@ -1106,6 +1517,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
+    std::vector<LevelTiming> timing;
     g->level_dirs.clear();
     g->level_cum_ms.clear();
     g->level_stats.clear();
@@ -1118,7 +1530,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 dir = BFSX_DIR_TOPDOWN;
             }
         }
-        if ((int)ws->ev_level.size() <= level) {
+        while ((int)ws->ev_level.size() <= level) {
             hipEvent_t e0, e1;
             BFSX_HIP_TRY(hipEventCreate(&e0));
             BFSX_HIP_TRY(hipEventCreate(&e1));
@@ -1148,6 +1560,40 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             in_queue = true;
         }
         snapped = false;
+        if (dir == BFSX_DIR_TOPDOWN && persist_fits(ctx, nf, dmax)) {
+            // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
+            const int ran = persist_td(g, ws, level, nf, mu);
+            if (ran < 0) return ran;
+            const PersistOut &po = *reinterpret_cast<const PersistOut *>(ws->h_pout);
+            for (int i = 0; i < ran; i++) {
+                const PersistRec &r = po.rec[i];
+                bfsx_level_stat ls{};
+                ls.direction = BFSX_DIR_TOPDOWN;
+                ls.level = level + i;
+                ls.frontier_in = nf;
+                ls.frontier_out = (int64_t)r.qtail;
+                ls.mf_in = (int64_t)r.scanned;
+                ls.unvisited_in = nv - visited - ws->n_dead;
+                ls.scanned = (int64_t)r.scanned;
+                ls.claims = (int64_t)r.claims;
+                g->level_stats.push_back(ls);
+                g->level_dirs.push_back(BFSX_DIR_TOPDOWN);
+                timing.push_back({level, true, (double)(r.t_end - po.t0) / ws->clock_khz,
+                                  (double)(r.t_end - (i ? po.rec[i - 1].t_end : po.t0)) / ws->clock_khz});
+                examined += ls.scanned;
+                visited += ls.frontier_out;
+                mu -= (int64_t)r.mf;
+                prev_nf = nf;
+                nf = ls.frontier_out;
+                mf = (int64_t)r.mf;
+                dmax = (int64_t)r.dmax;
+            }
+            std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
+            td_levels += ran;
+            level += ran - 1;
+            if (nf == 0) break;
+            continue;
+        }
         if (dir == BFSX_DIR_TOPDOWN) {
             // a wide top-down level may hand over to bottom-up: snapshot the visited bitmap (8 B per 64
             // vertices) so its frontier bitmap is one XOR pass instead of one atomic per discovered vertex
@@ -1184,6 +1630,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         ls.scanned = s.sc;
         ls.claims = s.cl;
         g->level_stats.push_back(ls);
+        timing.push_back({level, false, 0.0, 0.0});
         examined += ls.scanned;
         visited += nf_new;
         prev_nf = nf;
@@ -1213,8 +1660,15 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     g->level_cum_ms.resize(levels);
     for (int l = 0; l < levels; l++) {
         float t = 0.f, k = 0.f;
-        BFSX_HIP_TRY(hipEventElapsedTime(&t, ws->ev_start, ws->ev_level[l]));
-        BFSX_HIP_TRY(hipEventElapsedTime(&k, ws->ev_begin[l], ws->ev_level[l]));
+        const LevelTiming &lt = timing[l];
+        if (lt.persisted) { // device clock inside the launch that started at event slot lt.ev
+            BFSX_HIP_TRY(hipEventElapsedTime(&t, ws->ev_start, ws->ev_begin[lt.ev]));
+            t += (float)lt.rel_ms;
+            k = (float)lt.k_ms;
+        } else {
+            BFSX_HIP_TRY(hipEventElapsedTime(&t, ws->ev_start, ws->ev_level[l]));
+            BFSX_HIP_TRY(hipEventElapsedTime(&k, ws->ev_begin[l], ws->ev_level[l]));
+        }
         g->level_cum_ms[l] = t;
         g->level_stats[l].cum_ms = t;
         g->level_stats[l].kernel_ms = k;

@@ -92,7 +92,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "row_order" = degree|id (adjacency order inside a CSR row for graphs built afterwards; default
  *                 degree = high-degree neighbours first, which shortens bottom-up probes)
  *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
- *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS) */
+ *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS)
+ *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
+ *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU; fixed at a graph's first BFS) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */

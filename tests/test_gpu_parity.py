@@ -189,6 +189,57 @@ def test_row_order_option(ctx, order):
         ctx.set_option("row_order", "degree")
 
 
+@pytest.mark.parametrize("blocks", ["auto", "3"])
+@pytest.mark.parametrize("case", ["path", "grid", "kron", "lollipop"])
+def test_persistent_topdown_matches_per_level_kernels(ctx, case, blocks):
+    """K3p (narrow frontiers, many levels per launch) against the per-level kernels and the oracle:
+    identical distances, level counts, per-level frontier sizes, monotone level times; two sources per
+    graph (the barrier counters carry over between launches).  blocks: K3p workgroups (auto = one per CU;
+    3 = uneven slices, several steps per slice).  lollipop: a path into a 20000-leaf star, whose hub
+    must hand back to the per-level kernels (a slice could overflow its output segment)."""
+    if case == "path":
+        nv = 5000
+        u, v = np.arange(nv - 1), np.arange(1, nv)          # 5000 levels: five K3p launches
+    elif case == "grid":
+        side = 120
+        idx = np.arange(side * side).reshape(side, side)
+        u = np.r_[idx[:, :-1].ravel(), idx[:-1, :].ravel()]
+        v = np.r_[idx[:, 1:].ravel(), idx[1:, :].ravel()]
+        nv = side * side
+    elif case == "lollipop":
+        plen, leaves = 300, 20000
+        nv = plen + leaves
+        u = np.r_[np.arange(plen - 1), np.full(leaves, plen - 1), np.arange(plen, plen + 50)]
+        v = np.r_[np.arange(1, plen), np.arange(plen, nv), np.arange(plen + 1, plen + 51)]
+    else:
+        u, v = O.kronecker(14, 16, 99)
+        nv = 1 << 14
+    u = np.asarray(u, np.uint32)
+    v = np.asarray(v, np.uint32)
+    off, col = O.build_sets(nv, u, v)
+    srcs = [int(u[0]), int(v[len(v) // 2])]
+    refs = [O.csr_bfs(nv, off, col, s)[0] for s in srcs]
+    res = {}
+    try:
+        ctx.set_option("persist_blocks", blocks)
+        for mode in ("off", "on"):
+            ctx.set_option("persist", mode)
+            with ctx.from_edges(nv, u, v) as g:
+                for src, ref in zip(srcs, refs):
+                    d, p, st = g.bfs(src)
+                    assert np.array_equal(d, ref)
+                    assert O.validate(nv, off, col, src, d, p) == 0
+                    t = g.level_times()
+                    assert len(t) == st["levels"] and np.all(np.diff(t) >= 0)
+                    res[mode, src] = [(l["direction"], l["frontier_in"], l["frontier_out"])
+                                      for l in g.level_stats(1 << 14)]
+    finally:
+        ctx.set_option("persist", "on")
+        ctx.set_option("persist_blocks", "auto")
+    for src in srcs:
+        assert res["on", src] == res["off", src]
+
+
 @pytest.mark.parametrize("bits", ["auto", "64"])
 def test_offset_width_paths(ctx, bits):
     """uint32 and int64 row-offset instantiations of every traversal kernel agree with the oracle (int64

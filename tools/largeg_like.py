@@ -46,6 +46,7 @@ def write_graph(path, side=1000, m=7_586_063, radius=2, seed=2026):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="/tmp/largeG_like.txt")
+    ap.add_argument("--option", action="append", default=[], help="libbfsx option key=value")
     a = ap.parse_args()
     t0 = time.perf_counter()
     nv, m = write_graph(a.out)
@@ -55,6 +56,9 @@ def main():
     _, hu, hv = bfsx.parse_algs4(a.out)
     res["host_parse_s"] = round(time.perf_counter() - t0, 3)
     with bfsx.Context(0) as ctx:
+        for kv in a.option:
+            ctx.set_option(*kv.split("=", 1))
+        res["options"] = a.option
         ctx.parse_algs4_gpu(a.out)  # warm-up (code objects, allocator)
         t0 = time.perf_counter()
         _, gu, gv = ctx.parse_algs4_gpu(a.out)
