@@ -11,7 +11,7 @@ OBJDIR   := $(PKG)/build
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result -I include
 CXXFLAGS ?= -O2 -std=c++17 -Wall -I include
 
-KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip $(CSRC)/kernels_parse.hip
+KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip $(CSRC)/kernels_parse.hip $(CSRC)/kernels_validate.hip
 HOST_SRCS   := $(CSRC)/bfsx_api.cpp $(CSRC)/bfsx_comm.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 

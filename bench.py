@@ -159,10 +159,14 @@ def run_single(args):
     nv, nwords = g.nv, (g.nv + 63) // 64
     roots = g.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)
     # untimed pass: m_comp per root (Graph500 counts input tuples inside the root's component)
-    mcomp = {}
+    # and Graph500-style validation of every root's result on the device (bfsx_validate: a result that
+    # passes holds exactly the graph's BFS distances)
+    mcomp, val_errors = {}, 0
     for r in roots:
         _, _, st = g.bfs(int(r), want_dist=False, want_parent=False)
         mcomp[int(r)] = st["m_comp"]
+        val_errors += g.validate()["errors"]
+    assert val_errors == 0, f"validation failed: {val_errors} violating vertices"
     order = [int(roots[i % len(roots)]) for i in range(args.warmup + args.steps)]
     for r in order[: args.warmup]:
         g.bfs_device_only(r)
@@ -222,6 +226,8 @@ def run_single(args):
                            "achieved_GBs": round(bfs_ach, 1), "frac": round(bfs_ach / PEAK_HBM_GBS, 4)}
     out.update({"t_bfs_ms_mean": float(np.mean(t_bfs)), "t_bfs_ms_min": float(np.min(t_bfs)),
                 "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])), "graph_build_s": round(build_s, 3),
+                "validation": {"roots": len(roots), "errors": val_errors,
+                               "rules": "Graph500 kernel-2 + BreadthFirstPaths.check, on device (bfsx_validate)"},
                 "cpu_baseline": cpu})
     if args.levels_json:
         with open(args.levels_json, "w") as f:
@@ -253,7 +259,11 @@ def run_dist(args, world, rank, local_rank):
     build_s = time.perf_counter() - t0
     part = g.partition()
     roots = [int(r) for r in g.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)]
-    mcomp = {r: g.dist_bfs(r)["m_comp"] for r in roots}  # untimed, collective
+    mcomp, val_errors = {}, 0
+    for r in roots:  # untimed, collective: m_comp and Graph500-style validation of every root
+        mcomp[r] = g.dist_bfs(r)["m_comp"]
+        val_errors += g.validate()["errors"]
+    assert val_errors == 0, f"validation failed: {val_errors} violating vertices"
     order = [roots[i % len(roots)] for i in range(args.warmup + args.steps)]
     for r in order[: args.warmup]:
         g.dist_bfs(r, want_stats=False)
@@ -297,6 +307,8 @@ def run_dist(args, world, rank, local_rank):
                     "t_bfs_dev_ms_rank0_mean": float(np.mean([x[1] for x in local])),
                     "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])),
                     "graph_build_s": round(build_s, 3), "cpu_baseline": None,
+                    "validation": {"roots": len(roots), "errors": val_errors,
+                                   "rules": "Graph500 kernel-2 + BreadthFirstPaths.check, on device, collective"},
                     "levels_last": [{k: ls[k] for k in ("level", "direction", "frontier_in", "frontier_out",
                                                         "kernel_ms")} for ls in g.level_stats(256)]})
         print(json.dumps(out), flush=True)

@@ -33,7 +33,7 @@ EXPORTS = [
     "bfsx_graph_kronecker", "bfsx_kronecker_edges", "bfsx_graph_free", "bfsx_graph_nv",
     "bfsx_graph_nnz", "bfsx_graph_m", "bfsx_graph_csr", "bfsx_sample_roots", "bfsx_bfs",
     "bfsx_result", "bfsx_level_times", "bfsx_level_dirs", "bfsx_level_stats",
-    "bfsx_device_synchronize",
+    "bfsx_device_synchronize", "bfsx_validate", "bfsx_validate_result",
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
     "bfsx_dist_begin", "bfsx_dist_frontier_info", "bfsx_dist_td_expand", "bfsx_dist_td_claim",
     "bfsx_dist_frontier_slice", "bfsx_dist_bu_step", "bfsx_dist_level_end", "bfsx_dist_finish",
@@ -106,6 +106,8 @@ def lib():
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
         L.bfsx_device_synchronize.argtypes = [_VP]
         I64P = C.POINTER(C.c_int64)
+        L.bfsx_validate.argtypes = [_VP, C.c_int64, I64P, I64P, I64P, I64P]
+        L.bfsx_validate_result.argtypes = [_VP, C.c_int64, _VP, _VP, I64P, I64P]
         L.bfsx_dist_graph_from_edges.argtypes = [_VP, C.c_int64, _VP, _VP, C.c_int64, C.c_int, C.c_int,
                                                  C.POINTER(_VP)]
         L.bfsx_dist_graph_kronecker.argtypes = [_VP, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int, C.POINTER(_VP)]
@@ -302,6 +304,23 @@ class Graph:
         parent = np.empty(self.nv, np.int64)
         _check(lib().bfsx_result(self._h, _p(dist), _p(parent)))
         return dist, parent
+
+    def validate(self, source=-1):
+        """Graph500-style validation of the most recent BFS on the device (collective on a partitioned
+        graph).  Returns {errors, first_bad, reached, entries}; errors == 0 means the distances are
+        exactly the graph's BFS distances and the parents form a valid BFS tree."""
+        e, f, r, n = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        _check(lib().bfsx_validate(self._h, source, C.byref(e), C.byref(f), C.byref(r), C.byref(n)))
+        return {"errors": e.value, "first_bad": f.value, "reached": r.value, "entries": n.value}
+
+    def validate_result(self, source, dist, parent):
+        """Validate a caller-supplied (dist, parent) for this graph's rows.  Returns (errors, first_bad)."""
+        dist = np.ascontiguousarray(dist, np.int32)
+        parent = np.ascontiguousarray(parent, np.int64)
+        assert len(dist) == self.nv and len(parent) == self.nv
+        e, f = C.c_int64(), C.c_int64()
+        _check(lib().bfsx_validate_result(self._h, source, _p(dist), _p(parent), C.byref(e), C.byref(f)))
+        return e.value, f.value
 
     def level_times(self, cap=1 << 20):
         buf = np.empty(cap, np.float64)

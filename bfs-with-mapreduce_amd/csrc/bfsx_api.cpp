@@ -646,6 +646,39 @@ int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_o
     return BFSX_OK;
 }
 
+int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first_bad, int64_t *reached,
+                  int64_t *entries) {
+    if (!g) return fail(BFSX_E_ARG, "null graph");
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    int64_t res[4] = {0, -1, 0, 0};
+    if (int rc = bfs_validate(g, source, nullptr, res)) return rc;
+    if (errors) *errors = res[0];
+    if (first_bad) *first_bad = res[1];
+    if (reached) *reached = res[2];
+    if (entries) *entries = res[3];
+    return BFSX_OK;
+}
+
+int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, const int64_t *parent, int64_t *errors,
+                         int64_t *first_bad) {
+    if (!g || !dist || !parent) return fail(BFSX_E_ARG, "null argument");
+    BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    std::vector<unsigned long long> packed((size_t)g->nv);
+    for (int64_t i = 0; i < g->nv; i++)
+        packed[i] = ((unsigned long long)(uint32_t)parent[i] << 32) | (uint32_t)dist[i];
+    unsigned long long *d = nullptr;
+    BFSX_HIP_TRY(hipMalloc(&d, std::max<size_t>(packed.size(), 1) * sizeof(unsigned long long)));
+    hipError_t he = hipMemcpy(d, packed.data(), packed.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+    int64_t res[4] = {0, -1, 0, 0};
+    int rc = he == hipSuccess ? bfs_validate(g, source, d, res)
+                              : fail(BFSX_E_HIP, std::string("validate upload: ") + hipGetErrorString(he));
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (errors) *errors = res[0];
+    if (first_bad) *first_bad = res[1];
+    return BFSX_OK;
+}
+
 int bfsx_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));

@@ -83,6 +83,13 @@ int dist_finish(bfsx_graph *g);
 // the whole partitioned level loop with the exchanges through ctx->comm (collective over the ranks)
 int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 void bfs_workspace_free(BfsWorkspace *ws);
+// packed state (parent << 32 | dist) of the most recent BFS (device; null before the first one)
+const unsigned long long *bfs_state(const bfsx_graph *g);
+// ---- kernels_validate.hip: Graph500-style validation of the most recent result --------------------
+// res = {violating vertices, smallest violating id (-1: none), reached, adjacency entries checked};
+// collective on a partitioned graph.  stt: packed states of the local rows to check (device), null =
+// the most recent BFS (source < 0: its source).
+int bfs_validate(bfsx_graph *g, int64_t source, const unsigned long long *stt, int64_t res[4]);
 
 } // namespace bfsx
 

@@ -1699,6 +1699,8 @@ int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached) {
     return BFSX_OK;
 }
 
+const unsigned long long *bfs_state(const bfsx_graph *g) { return g->ws ? g->ws->st : nullptr; }
+
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     BfsWorkspace *ws = g->ws;
     if (!ws || g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");

@@ -151,6 +151,22 @@ int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap);
 /* Per-level records of the most recent bfsx_bfs.  Returns the number written (<= cap). */
 int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap);
 
+/* Graph500-style validation of the most recent BFS result of g, on the device, at any size (the CPU
+ * oracle's orc_validate rules; Graph500 kernel-2 validation; algs4.jar!/BreadthFirstPaths.java:171-212
+ * `check`): dist[source] = 0 and parent[source] = source; every reached v has a parent joined to it by
+ * an edge with dist[parent] = dist[v] - 1; unreached vertices have no parent and no reached neighbour;
+ * every edge joins vertices whose distances differ by at most one.  A result that passes holds exactly
+ * the BFS distances of the graph.  errors = violating vertices (0 = valid), first_bad = smallest
+ * violating id (-1 = none), reached / entries = reached vertices / adjacency entries checked (any
+ * output may be NULL).  Collective on a partitioned graph (all-gathers the distances).  source < 0 =
+ * the source of the most recent BFS. */
+int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first_bad, int64_t *reached,
+                  int64_t *entries);
+/* The same rules on a caller-supplied result (host arrays of length bfsx_graph_nv: this rank's rows on a
+ * partitioned graph), e.g. one read back from a reference run or a file written by the host twin. */
+int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, const int64_t *parent,
+                         int64_t *errors, int64_t *first_bad);
+
 /* ---- multi-GPU: 1-D vertex partition -------------------------------------------
  * Replaces Spark's hash-partitioned reduceByKey shuffle (BfsSpark.java:90) with an owner-routed
  * exchange.  Rank r of P holds the rows of global ids [r*chunk, r*chunk + nv_local), chunk =
