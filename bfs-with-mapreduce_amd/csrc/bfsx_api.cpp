@@ -269,6 +269,24 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         }
         return as_int(ctx->opt.persist_blocks);
     }
+    if (k == "build_chunk") {
+        char *end = nullptr;
+        const long long x = strtoll(value, &end, 10);
+        if (!end || *end || x < 1) return fail(BFSX_E_ARG, "build_chunk must be a positive entry count");
+        ctx->opt.build_chunk = x;
+        return BFSX_OK;
+    }
+    if (k == "hub_bits") {
+        if (v == "auto") ctx->opt.hub_bits = -1;
+        else if (v == "off") ctx->opt.hub_bits = 0;
+        else {
+            int b = 0;
+            if (int rc = as_int(b)) return rc;
+            if (b < 1 || b > 30) return fail(BFSX_E_ARG, "hub_bits must be auto|off|1..30");
+            ctx->opt.hub_bits = b;
+        }
+        return BFSX_OK;
+    }
     if (k == "offset_bits") {
         if (v == "auto") ctx->opt.offset_bits = 0;
         else if (v == "64") ctx->opt.offset_bits = 64;
@@ -310,6 +328,7 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
                                    int nranks, bfsx_graph **out) {
     bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
     if (!g) return fail(BFSX_E_OOM, "graph");
+    set_build_chunk(ctx->opt.build_chunk);
     int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, &g->d_row_off, &g->d_col,
                               &g->nnz, &g->d_tuple_cnt, g->v_lo, nv);
     if (rc) {
@@ -431,6 +450,7 @@ static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t se
     // built straight from the counter stream: no tuple arrays (8 B per tuple, 137 GB at scale 30)
     bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
     if (!g) return fail(BFSX_E_OOM, "graph");
+    set_build_chunk(ctx->opt.build_chunk);
     int rc = build_csr_kronecker(ctx->stream, scale, edgefactor, seed, ctx->opt.degree_order, &g->d_row_off,
                                  &g->d_col, &g->nnz, &g->d_tuple_cnt, g->v_lo, g->nv);
     (void)hipStreamSynchronize(ctx->stream);

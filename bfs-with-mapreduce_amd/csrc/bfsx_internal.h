@@ -32,6 +32,8 @@ struct Options {
     int persist_blocks = 0;     // K3p workgroups (0: one per CU)
     int offset_bits = 0;        // traversal row-offset width: 0 = uint32 when nnz < 2^32, else int64; 64 = int64
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
+    int hub_bits = -1;          // bottom-up hub probe domain: -1 auto, 0 off, b = 2^b hubs
+    int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------
@@ -54,6 +56,8 @@ struct Comm {
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
                      bool degree_order, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
                      uint32_t **d_tuple_cnt, int64_t lo = 0, int64_t nv_global = -1);
+// Row-chunk size (raw adjacency entries) of the CSR build's sort/dedup/ordering passes, calling thread.
+void set_build_chunk(int64_t entries);
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v);
 // ---- kernels_parse.hip: GPU tokenizer of the algs4 edge lines (after the two header lines) -----

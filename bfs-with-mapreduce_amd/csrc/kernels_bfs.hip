@@ -20,6 +20,8 @@
 #include <chrono>
 #include <type_traits>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "bfsx_internal.h"
 
 namespace bfsx {
@@ -82,6 +84,12 @@ struct BfsWorkspace {
     int64_t n_dead = 0;                 // isolated vertices (excluding padding)
     uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex (+ kDeg1 flag)
     uint32_t top1_flag = 0;             // kDeg1 when every global id < 2^31, else 0 (flag unused)
+    // hub-encoded probe domain of the bottom-up kernel (single device; see k_bu): the hub_k highest-degree
+    // vertices, their frontier bits gathered into a small bitmap per bottom-up level
+    int64_t hub_k = 0;                  // 0: off
+    uint32_t *hub_id = nullptr;         // [hub_k] global id of hub h (degree descending)
+    uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
+    u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
     LevelSlot *ring = nullptr;          // device, 3 slots
     LevelSlot *h_slot = nullptr;        // pinned host mirror of one slot
@@ -914,15 +922,39 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ 
 // level is only ever followed by the n_f test), so the level accumulates the exact m_u instead --
 // the degree sum of the candidates it leaves unvisited, which it reads anyway.  kMf (multi-GPU)
 // also accumulates m_f, the size bound of the next top-down exchange.
+// kHubs (single device): every frontier-bit probe of the level is a random 8-B access into an n/8-byte
+// bitmap (8 MiB at scale 26: twice an XCD's L2, so most probes are served by the Infinity Cache).  The
+// probes concentrate on high-degree vertices: top1 IS a vertex's highest-degree neighbour and rows are
+// degree-ordered.  So the hub_k highest-degree vertices get a second, dense id h: `colh` (a copy of col)
+// and top1 carry kHubBit | h for hub entries, and a kernel before each bottom-up level gathers the
+// hubs' frontier bits into `hfront` (hub_k bits: 256 KiB at scale 26, L2-resident on every XCD).  A
+// hub probe reads hfront, any other probe reads front; the parent of a hub hit is hub_id[h].
 constexpr int kBuU = 4;
 constexpr int kBuRound = 64 * kBuU;
 constexpr uint32_t kDeg1 = 0x80000000u;
+constexpr uint32_t kHubBit = 0x40000000u; // hub encoding needs every global id < 2^30
+constexpr uint32_t kHubMask = kHubBit - 1u;
 
-template <class OffT, bool kMf>
+// word holding the frontier bit of probe id x (bit x & 63: a hub index keeps the id's low 6 bits)
+template <bool kHubs>
+__device__ inline const u64 *probe_word(const u64 *__restrict__ front, const u64 *__restrict__ hfront, uint32_t x) {
+    if (kHubs) {
+        const bool hb = (x & kHubBit) != 0u;
+        return (hb ? hfront : front) + ((x & (hb ? kHubMask : 0xFFFFFFFFu)) >> 6);
+    }
+    return front + (x >> 6);
+}
+template <bool kHubs>
+__device__ inline uint32_t probe_id(const uint32_t *__restrict__ hub_id, uint32_t x) {
+    return (kHubs && (x & kHubBit)) ? hub_id[x & kHubMask] : x;
+}
+
+template <class OffT, bool kMf, bool kHubs>
 __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const u64 *__restrict__ front,
                                             u64 *__restrict__ next, u64 *__restrict__ vis, u64 *__restrict__ stt,
-                                            LevelSlot *ring, int level, int64_t nwords, uint32_t fmask) {
+                                            LevelSlot *ring, int level, int64_t nwords, uint32_t fmask,
+                                            const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
@@ -974,7 +1006,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
 #pragma unroll
                 for (int k = 0; k < kBuU; k++) {
                     const uint32_t id = x[k] & ~fmask;
-                    fw[k] = (t0 + (uint32_t)k * 64 + lane < he) ? front[id >> 6] : 0ull;
+                    fw[k] = (t0 + (uint32_t)k * 64 + lane < he) ? *probe_word<kHubs>(front, hfront, id) : 0ull;
                 }
                 uint32_t nmiss = 0; // wave-uniform
 #pragma unroll
@@ -985,7 +1017,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
                     const bool last = (x[k] & fmask) != 0; // top1 was the row's only entry
                     if (ok) acc_sc += 1;
                     if (hit) {
-                        stt[v[k]] = pack_state(id, nd);
+                        stt[v[k]] = pack_state(probe_id<kHubs>(hub_id, id), nd);
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
                         if (kMf) acc_mf += (u64)(row_off[v[k] + 1] - row_off[v[k]]);
@@ -1011,10 +1043,10 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
                             const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                             const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                             const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                            const bool h0 = (front[x0 >> 6] >> (x0 & 63u)) & 1ull;
-                            const bool h1 = (front[x1 >> 6] >> (x1 & 63u)) & 1ull;
-                            const bool h2 = (front[x2 >> 6] >> (x2 & 63u)) & 1ull;
-                            const bool h3 = (front[x3 >> 6] >> (x3 & 63u)) & 1ull;
+                            const bool h0 = (*probe_word<kHubs>(front, hfront, x0) >> (x0 & 63u)) & 1ull;
+                            const bool h1 = (*probe_word<kHubs>(front, hfront, x1) >> (x1 & 63u)) & 1ull;
+                            const bool h2 = (*probe_word<kHubs>(front, hfront, x2) >> (x2 & 63u)) & 1ull;
+                            const bool h3 = (*probe_word<kHubs>(front, hfront, x3) >> (x3 & 63u)) & 1ull;
                             if (h0 | h1 | h2 | h3) {
                                 found = true;
                                 const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
@@ -1027,7 +1059,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
                         acc_sc += (u64)(j - b - 1);
                         acc_rows += 1;
                         if (found) {
-                            stt[vv] = pack_state(par, nd);
+                            stt[vv] = pack_state(probe_id<kHubs>(hub_id, par), nd);
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
                             if (kMf) acc_mf += (u64)(e - b);
@@ -1170,6 +1202,43 @@ __global__ __launch_bounds__(kBS) void k_top1(const int64_t *__restrict__ row_of
     }
 }
 
+// Hub selection: sort keys ~degree (ascending = degree descending, ties by id: the sort is stable).
+__global__ __launch_bounds__(kBS) void k_hub_keys(const int64_t *__restrict__ row_off, int64_t nv,
+                                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
+        keys[v] = ~(uint32_t)(row_off[v + 1] - row_off[v]);
+        ids[v] = (uint32_t)v;
+    }
+}
+__global__ __launch_bounds__(kBS) void k_hub_index(const uint32_t *__restrict__ hub_id, int64_t k,
+                                                   uint32_t *__restrict__ hidx) {
+    for (int64_t h = (int64_t)blockIdx.x * kBS + threadIdx.x; h < k; h += (int64_t)gridDim.x * kBS)
+        hidx[hub_id[h]] = (uint32_t)h;
+}
+// out[i] = hub-encoded in[i] (bits in `keep` pass through: the top1 degree-1 flag); in == out allowed
+__global__ __launch_bounds__(kBS) void k_hub_encode(const uint32_t *in, int64_t n, const uint32_t *__restrict__ hidx,
+                                                    uint32_t keep, uint32_t *out) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        const uint32_t x = in[i];
+        const uint32_t h = hidx[x & ~keep];
+        out[i] = (h != 0xFFFFFFFFu ? (kHubBit | h) : (x & ~keep)) | (x & keep);
+    }
+}
+// Before a bottom-up level: hfront bit h = frontier bit of hub h (one lane per hub, a ballot per word).
+__global__ __launch_bounds__(kBS) void k_hub_gather(const uint32_t *__restrict__ hub_id, int64_t k,
+                                                    const u64 *__restrict__ front, u64 *__restrict__ hfront) {
+    for (int64_t h0 = (int64_t)blockIdx.x * kBS; h0 < k; h0 += (int64_t)gridDim.x * kBS) {
+        const int64_t h = h0 + threadIdx.x;
+        bool bit = false;
+        if (h < k) {
+            const uint32_t v = hub_id[h];
+            bit = (front[v >> 6] >> (v & 63u)) & 1ull;
+        }
+        const u64 w = __ballot(bit);
+        if ((threadIdx.x & 63u) == 0 && h < k) hfront[h >> 6] = w;
+    }
+}
+
 __global__ __launch_bounds__(kBS) void k_off32(const int64_t *__restrict__ row_off, int64_t n,
                                                uint32_t *__restrict__ off32) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS)
@@ -1229,6 +1298,69 @@ unsigned clamp_grid(int64_t blocks, unsigned cap) {
     return (unsigned)std::min<int64_t>(blocks, cap);
 }
 
+// Hub probe domain of k_bu (single device): the hub_k highest-degree vertices (option "hub_bits":
+// auto = the power of two >= n/1024 (measured: 2^16..2^19 hubs at scale 26 within noise, more hubs slower
+// as the per-level gather grows), off for graphs partitioned over several ranks, ids >= 2^30 or
+// n < 2^16).  The hub ranking needs every vertex's degree, which a rank of a partition does not hold.
+int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
+    const int hb = g->ctx->opt.hub_bits;
+    if (g->nranks > 1 || hb == 0 || g->nv_global > ((int64_t)1 << 30) || g->nv < 64) return BFSX_OK;
+    int64_t k;
+    if (hb < 0) {
+        if (g->nv < ((int64_t)1 << 16)) return BFSX_OK;
+        k = 64;
+        while (k * 1024 < g->nv) k *= 2;
+    } else {
+        k = (int64_t)1 << hb;
+    }
+    k = std::min<int64_t>(k, g->nv);
+    hipStream_t st = g->ctx->stream;
+    const size_t nv = (size_t)g->nv;
+    // the encoded adjacency copy (4 B per entry) and the ranking temporaries must leave half of the free
+    // device memory untouched (scale 30 on one device: the graph alone is ~150 GB), else stay off
+    size_t mfree = 0, mtotal = 0;
+    BFSX_HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
+    if ((size_t)g->nnz * 4 + nv * 20 > mfree / 2) return BFSX_OK;
+    struct Tmp {
+        void *p = nullptr;
+        ~Tmp() {
+            if (p) (void)hipFree(p);
+        }
+    } keys, keys2, ids, ids2, hidx, sort_tmp;
+    BFSX_HIP_TRY(hipMalloc(&keys.p, nv * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&keys2.p, nv * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&ids.p, nv * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&ids2.p, nv * sizeof(uint32_t)));
+    const unsigned gfill = clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192);
+    hipLaunchKernelGGL(k_hub_keys, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, (uint32_t *)keys.p,
+                       (uint32_t *)ids.p);
+    BFSX_HIP_TRY(hipGetLastError());
+    size_t tb = 0;
+    BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
+                                           (uint32_t *)ids2.p, nv, 0, 32, st));
+    BFSX_HIP_TRY(hipMalloc(&sort_tmp.p, std::max<size_t>(tb, 16)));
+    BFSX_HIP_TRY(rocprim::radix_sort_pairs(sort_tmp.p, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
+                                           (uint32_t *)ids2.p, nv, 0, 32, st));
+    BFSX_HIP_TRY(hipMalloc(&ws->hub_id, (size_t)k * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->hub_id, ids2.p, (size_t)k * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    BFSX_HIP_TRY(hipMalloc(&hidx.p, nv * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMemsetAsync(hidx.p, 0xFF, nv * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_hub_index, dim3(clamp_grid((k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->hub_id, k,
+                       (uint32_t *)hidx.p);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipMalloc(&ws->colh, (size_t)std::max<int64_t>(g->nnz, 1) * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid((g->nnz + kBS - 1) / kBS, 65536)), dim3(kBS), 0, st, g->d_col,
+                       g->nnz, (const uint32_t *)hidx.p, 0u, ws->colh);
+    BFSX_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_encode, dim3(gfill), dim3(kBS), 0, st, ws->top1, g->nv, (const uint32_t *)hidx.p,
+                       ws->top1_flag, ws->top1);
+    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipMalloc(&ws->hfront, (size_t)((k + 63) / 64) * sizeof(u64)));
+    BFSX_HIP_TRY(hipStreamSynchronize(st)); // the temporaries are freed on return
+    ws->hub_k = k;
+    return BFSX_OK;
+}
+
 int ws_alloc(bfsx_graph *g) {
     if (g->ws) return BFSX_OK;
     auto *ws = new BfsWorkspace();
@@ -1269,6 +1401,7 @@ int ws_alloc(bfsx_graph *g) {
     ws->top1_flag = (g->nv_global <= ((int64_t)1 << 31)) ? kDeg1 : 0u;
     hipLaunchKernelGGL(k_top1, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->d_col, g->nv, ws->top1_flag, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
+    if (int e = hub_setup(g, ws)) return e;
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
                        g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
     BFSX_HIP_TRY(hipGetLastError());
@@ -1319,27 +1452,38 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     return BFSX_OK;
 }
 
-template <bool kMf>
-int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
+template <class OffT, bool kMf, bool kHubs>
+int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
     hipStream_t st = g->ctx->stream;
     // persistent grid: exactly the resident workgroups (a partial second wave of workgroups would
     // leave most CUs idle at the tail of the grid-stride loop)
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<uint32_t, kMf>, kBS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs>, kBS, 0) != hipSuccess ||
             per_cu < 1)
             per_cu = 4;
     }
     const unsigned cap = (unsigned)(g->ctx->num_cus * per_cu);
     const dim3 grid(clamp_grid((ws->nwords + kWaves * 64 - 1) / (kWaves * 64), cap));
-    if (ws->off32)
-        hipLaunchKernelGGL((k_bu<uint32_t, kMf>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->top1, front,
-                           ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag);
-    else
-        hipLaunchKernelGGL((k_bu<int64_t, kMf>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->top1, front,
-                           ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag);
+    if (kHubs) {
+        hipLaunchKernelGGL(k_hub_gather, dim3(clamp_grid((ws->hub_k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                           ws->hub_id, ws->hub_k, front, ws->hfront);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
+                       ws->top1, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag,
+                       ws->hfront, ws->hub_id);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
+}
+
+template <bool kMf>
+int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
+    if (ws->hub_k > 0) // top1 is hub-encoded: every bottom-up launch of this graph uses the hub domain
+        return ws->off32 ? launch_bu_t<uint32_t, kMf, true>(g, ws, ws->off32, front, level)
+                         : launch_bu_t<int64_t, kMf, true>(g, ws, g->d_row_off, front, level);
+    return ws->off32 ? launch_bu_t<uint32_t, kMf, false>(g, ws, ws->off32, front, level)
+                     : launch_bu_t<int64_t, kMf, false>(g, ws, g->d_row_off, front, level);
 }
 
 struct SlotSums {
@@ -1472,7 +1616,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
         if (p) (void)hipFree(p);
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
-                    (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
+                    (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr})
         if (p) (void)hipFree(p);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);

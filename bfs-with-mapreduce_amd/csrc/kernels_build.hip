@@ -28,6 +28,14 @@ namespace {
 
 constexpr int kBS = 256;
 
+// raw adjacency entries per build chunk (option "build_chunk"; set per build by the calling thread)
+thread_local int64_t kBuildChunk = (int64_t)1 << 30;
+
+__global__ void k_fill_i64(int64_t *__restrict__ p, int64_t n, int64_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
 inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap = 16384) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -156,14 +164,6 @@ __global__ __launch_bounds__(kBS) void k_count_all(Src src, int64_t m, uint32_t 
     }
 }
 
-__global__ __launch_bounds__(kBS) void k_mark_heads(const int64_t *__restrict__ off, int64_t nv,
-                                                    uint8_t *__restrict__ keep) {
-    for (int64_t r = (int64_t)blockIdx.x * kBS + threadIdx.x; r < nv; r += (int64_t)gridDim.x * kBS) {
-        int64_t b = off[r];
-        if (off[r + 1] > b) keep[b] = 1;
-    }
-}
-
 __global__ __launch_bounds__(kBS) void k_keep(const uint32_t *__restrict__ col, int64_t nnz,
                                               uint8_t *__restrict__ keep) {
     for (int64_t j = (int64_t)blockIdx.x * kBS + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * kBS) {
@@ -179,10 +179,20 @@ __global__ __launch_bounds__(kBS) void k_compact(const uint32_t *__restrict__ co
         if (keep[j]) out[pos[j]] = col[j];
 }
 
-__global__ __launch_bounds__(kBS) void k_new_off(const int64_t *__restrict__ off, const int64_t *__restrict__ pos,
-                                                 int64_t nv, int64_t *__restrict__ noff) {
-    for (int64_t r = (int64_t)blockIdx.x * kBS + threadIdx.x; r <= nv; r += (int64_t)gridDim.x * kBS)
-        noff[r] = pos[off[r]];
+// Chunk variants (rows [r0, r1) whose raw entries are [e0, e1)): heads relative to e0, and the new row
+// offsets = the chunk's output base + the rank of the row's first entry among the kept ones.
+__global__ __launch_bounds__(kBS) void k_mark_heads_c(const int64_t *__restrict__ off, int64_t r0, int64_t r1,
+                                                      int64_t e0, uint8_t *__restrict__ keep) {
+    for (int64_t r = r0 + (int64_t)blockIdx.x * kBS + threadIdx.x; r < r1; r += (int64_t)gridDim.x * kBS) {
+        const int64_t b = off[r];
+        if (off[r + 1] > b) keep[b - e0] = 1;
+    }
+}
+__global__ __launch_bounds__(kBS) void k_new_off_c(const int64_t *__restrict__ off, const int64_t *__restrict__ pos,
+                                                   int64_t r0, int64_t r1, int64_t e0, int64_t obase,
+                                                   int64_t *__restrict__ noff) {
+    for (int64_t r = r0 + (int64_t)blockIdx.x * kBS + threadIdx.x; r < r1; r += (int64_t)gridDim.x * kBS)
+        noff[r] = obase + pos[off[r] - e0];
 }
 
 struct SubBase {
@@ -214,6 +224,8 @@ struct DevBuf {
 
 } // namespace
 
+void set_build_chunk(int64_t entries) { kBuildChunk = std::max<int64_t>(entries, 1); }
+
 int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t seed, uint32_t *d_u,
                        uint32_t *d_v) {
     const KronParams p = kron_params(scale, seed);
@@ -223,53 +235,37 @@ int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t s
     return BFSX_OK;
 }
 
-// Segmented radix sort of every CSR row (keys_in -> keys_out), in row chunks of < 2^31 entries
-// (rocPRIM's segmented sort takes 32-bit sizes).
+// Row chunks [cuts[i], cuts[i+1]) of at most `limit` entries each (a longer single row is a chunk of
+// its own), from a host copy of the offsets.
+int plan_row_chunks(const std::vector<int64_t> &h_off, int64_t nv, int64_t limit, std::vector<int64_t> &cuts) {
+    cuts.assign(1, 0);
+    int64_t r = 0;
+    while (r < nv) {
+        int64_t r2 = std::upper_bound(h_off.begin() + r, h_off.begin() + nv + 1, h_off[r] + limit) - h_off.begin() - 1;
+        if (r2 <= r) r2 = r + 1; // one row longer than the limit
+        if (h_off[r2] - h_off[r] >= ((int64_t)1 << 31)) return fail(BFSX_E_ARG, "a single adjacency row exceeds 2^31 entries");
+        r2 = std::min<int64_t>(r2, nv);
+        cuts.push_back(r2);
+        r = r2;
+    }
+    return BFSX_OK;
+}
+
+// One segmented sort of `rows` rows (offsets d_off[0..rows], entries starting at e0; n < 2^31 entries):
+// keys_in[0..n) -> keys_out[0..n).
 template <class K>
-int sort_rows(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz, const K *keys_in, K *keys_out,
-              unsigned end_bit) {
-    if (nnz <= 0) return BFSX_OK;
-    std::vector<int64_t> h_off;
-    const int64_t kChunk = (int64_t)1 << 31;
-    std::vector<int64_t> row_cuts{0};
-    if (nnz >= kChunk) {
-        h_off.resize(nv + 1);
-        BFSX_HIP_TRY(hipMemcpy(h_off.data(), d_off, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-        int64_t r = 0;
-        while (r < nv) {
-            const int64_t limit = h_off[r] + kChunk - 1;
-            int64_t r2 = std::upper_bound(h_off.begin() + r, h_off.end(), limit) - h_off.begin() - 1;
-            if (r2 <= r) return fail(BFSX_E_ARG, "a single adjacency row exceeds 2^31 entries");
-            r2 = std::min<int64_t>(r2, nv);
-            row_cuts.push_back(r2);
-            r = r2;
-        }
-    } else {
-        row_cuts.push_back(nv);
-    }
+int sort_rows_range(hipStream_t stream, const int64_t *d_off, int64_t rows, int64_t e0, int64_t n, const K *keys_in,
+                    K *keys_out, unsigned end_bit) {
+    auto beg = rocprim::make_transform_iterator(d_off, SubBase{e0});
+    auto end = rocprim::make_transform_iterator(d_off + 1, SubBase{e0});
+    size_t tmp_bytes = 0;
+    BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, keys_in, keys_out, (unsigned)n,
+                                                    (unsigned)rows, beg, end, 0, end_bit, stream));
     DevBuf<char> tmp;
-    size_t tmp_cap = 0;
-    for (size_t c = 0; c + 1 < row_cuts.size(); c++) {
-        const int64_t r0 = row_cuts[c], r1 = row_cuts[c + 1];
-        const int64_t e0 = h_off.empty() ? 0 : h_off[r0];
-        const int64_t e1 = h_off.empty() ? nnz : h_off[r1];
-        if (e1 == e0) continue;
-        auto beg = rocprim::make_transform_iterator(d_off + r0, SubBase{e0});
-        auto end = rocprim::make_transform_iterator(d_off + r0 + 1, SubBase{e0});
-        size_t tmp_bytes = 0;
-        BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, keys_in + e0, keys_out + e0,
-                                                        (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end, 0,
-                                                        end_bit, stream));
-        if (tmp_bytes > tmp_cap) {
-            tmp.reset();
-            BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
-            tmp_cap = tmp_bytes;
-        }
-        BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(tmp.p, tmp_bytes, keys_in + e0, keys_out + e0,
-                                                        (unsigned)(e1 - e0), (unsigned)(r1 - r0), beg, end, 0,
-                                                        end_bit, stream));
-    }
-    BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
+    BFSX_HIP_TRY(rocprim::segmented_radix_sort_keys(tmp.p, tmp_bytes, keys_in, keys_out, (unsigned)n, (unsigned)rows,
+                                                    beg, end, 0, end_bit, stream));
+    BFSX_HIP_TRY(hipStreamSynchronize(stream)); // tmp is freed on return
     return BFSX_OK;
 }
 
@@ -293,20 +289,29 @@ __global__ __launch_bounds__(kBS) void k_low32(const unsigned long long *__restr
 }
 
 // Re-order every row so that high-degree neighbours come first: a bottom-up probe of an unvisited
-// vertex then tests the neighbour most likely to be in a large frontier first (early exit).
+// vertex then tests the neighbour most likely to be in a large frontier first (early exit).  Row chunks
+// of <= kBuildChunk entries keep the 64-bit sort keys at 16 B per CHUNK entry, not per graph entry.
 int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, int64_t nnz, uint32_t *d_col,
                          const uint32_t *gdeg) {
     if (nnz <= 0) return BFSX_OK;
+    std::vector<int64_t> h_off(nv + 1), cuts;
+    BFSX_HIP_TRY(hipMemcpy(h_off.data(), d_off, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (int rc = plan_row_chunks(h_off, nv, kBuildChunk, cuts)) return rc;
+    int64_t cap = 0;
+    for (size_t c = 0; c + 1 < cuts.size(); c++) cap = std::max(cap, h_off[cuts[c + 1]] - h_off[cuts[c]]);
     DevBuf<unsigned long long> k0, k1;
-    BFSX_HIP_TRY(k0.alloc(nnz));
-    BFSX_HIP_TRY(k1.alloc(nnz));
-    hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(nnz, kBS)), dim3(kBS), 0, stream, d_off, d_col, gdeg, nnz,
-                       k0.p);
-    BFSX_HIP_TRY(hipGetLastError());
-    int rc = sort_rows(stream, d_off, nv, nnz, k0.p, k1.p, 64u);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_low32, dim3(grid_for(nnz, kBS)), dim3(kBS), 0, stream, k1.p, nnz, d_col);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(k0.alloc(cap));
+    BFSX_HIP_TRY(k1.alloc(cap));
+    for (size_t c = 0; c + 1 < cuts.size(); c++) {
+        const int64_t r0 = cuts[c], r1 = cuts[c + 1], e0 = h_off[r0], n = h_off[r1] - e0;
+        if (n <= 0) continue;
+        hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(n, kBS)), dim3(kBS), 0, stream, d_off, d_col + e0, gdeg, n,
+                           k0.p);
+        BFSX_HIP_TRY(hipGetLastError());
+        if (int rc = sort_rows_range(stream, d_off + r0, r1 - r0, e0, n, k0.p, k1.p, 64u)) return rc;
+        hipLaunchKernelGGL(k_low32, dim3(grid_for(n, kBS)), dim3(kBS), 0, stream, k1.p, n, d_col + e0);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
     BFSX_HIP_TRY(hipStreamSynchronize(stream));
     return BFSX_OK;
 }
@@ -360,58 +365,73 @@ int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degr
         BFSX_HIP_TRY(hipStreamSynchronize(stream));
     }
 
-    // K1d: sort every row by neighbour id
-    DevBuf<uint32_t> col_s;
-    BFSX_HIP_TRY(col_s.alloc(nnz_raw));
+    // K1d + K1e per row chunk (<= kBuildChunk raw entries): sort the chunk's rows by neighbour id into a
+    // chunk buffer, mark the first copy of every neighbour, scan, and compact the kept entries back into
+    // `col` at the running output position (never past the chunk's own start: dedup only shrinks), with
+    // the chunk's new row offsets.  Peak memory is the raw adjacency + ~13 B per chunk entry instead of
+    // ~21 B per graph entry, so a scale-30 graph builds on one 288 GB device.  `col` keeps its raw
+    // allocation (the few % of duplicates) instead of a copy to the exact size.
+    DevBuf<int64_t> noff;
+    BFSX_HIP_TRY(noff.alloc(nv + 1));
+    int64_t nnz = 0;
     {
+        std::vector<int64_t> h_off(nv + 1), cuts;
+        BFSX_HIP_TRY(hipMemcpy(h_off.data(), off.p, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (int rc = plan_row_chunks(h_off, nv, kBuildChunk, cuts)) return rc;
+        int64_t cap = 0;
+        for (size_t c = 0; c + 1 < cuts.size(); c++) cap = std::max(cap, h_off[cuts[c + 1]] - h_off[cuts[c]]);
         unsigned end_bit = 1;
         while (end_bit < 32 && (1ULL << end_bit) < (uint64_t)nv_global) end_bit++;
-        int rc = sort_rows(stream, off.p, nv, nnz_raw, col.p, col_s.p, end_bit);
-        if (rc) return rc;
+        DevBuf<uint32_t> col_s;
+        DevBuf<uint8_t> keep;
+        DevBuf<int64_t> pos;
+        BFSX_HIP_TRY(col_s.alloc(cap));
+        BFSX_HIP_TRY(keep.alloc(cap + 1));
+        BFSX_HIP_TRY(pos.alloc(cap + 1));
+        DevBuf<char> stmp;
+        size_t stmp_cap = 0;
+        for (size_t c = 0; c + 1 < cuts.size(); c++) {
+            const int64_t r0 = cuts[c], r1 = cuts[c + 1], e0 = h_off[r0], n = h_off[r1] - e0;
+            if (n > 0) {
+                if (int rc = sort_rows_range(stream, off.p + r0, r1 - r0, e0, n, col.p + e0, col_s.p, end_bit))
+                    return rc;
+                BFSX_HIP_TRY(hipMemsetAsync(keep.p, 0, n + 1, stream));
+                hipLaunchKernelGGL(k_mark_heads_c, dim3(grid_for(r1 - r0, kBS)), dim3(kBS), 0, stream, off.p, r0, r1,
+                                   e0, keep.p);
+                BFSX_HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_keep, dim3(grid_for(n, kBS)), dim3(kBS), 0, stream, col_s.p, n, keep.p);
+                BFSX_HIP_TRY(hipGetLastError());
+                auto in = rocprim::make_transform_iterator(keep.p, U8ToI64{});
+                size_t tb = 0;
+                BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, tb, in, pos.p, (int64_t)0, (size_t)(n + 1),
+                                                     rocprim::plus<int64_t>(), stream));
+                if (tb > stmp_cap) {
+                    stmp.reset();
+                    BFSX_HIP_TRY(stmp.alloc(tb));
+                    stmp_cap = tb;
+                }
+                BFSX_HIP_TRY(rocprim::exclusive_scan(stmp.p, tb, in, pos.p, (int64_t)0, (size_t)(n + 1),
+                                                     rocprim::plus<int64_t>(), stream));
+                hipLaunchKernelGGL(k_compact, dim3(grid_for(n, kBS)), dim3(kBS), 0, stream, col_s.p, keep.p, pos.p, n,
+                                   col.p + nnz);
+                BFSX_HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_new_off_c, dim3(grid_for(r1 - r0, kBS)), dim3(kBS), 0, stream, off.p, pos.p, r0,
+                                   r1, e0, nnz, noff.p);
+                BFSX_HIP_TRY(hipGetLastError());
+                int64_t kept = 0;
+                BFSX_HIP_TRY(hipMemcpyAsync(&kept, pos.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+                BFSX_HIP_TRY(hipStreamSynchronize(stream));
+                nnz += kept;
+            } else {
+                hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(r1 - r0, kBS)), dim3(kBS), 0, stream, noff.p + r0, r1 - r0,
+                                   nnz);
+                BFSX_HIP_TRY(hipGetLastError());
+            }
+        }
+        BFSX_HIP_TRY(hipMemcpyAsync(noff.p + nv, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, stream));
+        BFSX_HIP_TRY(hipStreamSynchronize(stream));
     }
-    col.reset(); // unsorted rows are no longer needed
-
-    // K1e: dedup
-    DevBuf<uint8_t> keep;
-    DevBuf<int64_t> pos;
-    BFSX_HIP_TRY(keep.alloc(nnz_raw + 1));
-    BFSX_HIP_TRY(pos.alloc(nnz_raw + 1));
-    BFSX_HIP_TRY(hipMemsetAsync(keep.p, 0, nnz_raw + 1, stream));
-    hipLaunchKernelGGL(k_mark_heads, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, off.p, nv, keep.p);
-    BFSX_HIP_TRY(hipGetLastError());
-    if (nnz_raw > 0) {
-        hipLaunchKernelGGL(k_keep, dim3(grid_for(nnz_raw, kBS)), dim3(kBS), 0, stream, col_s.p, nnz_raw, keep.p);
-        BFSX_HIP_TRY(hipGetLastError());
-    }
-    {
-        auto in = rocprim::make_transform_iterator(keep.p, U8ToI64{});
-        size_t tmp_bytes = 0;
-        BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, in, pos.p, (int64_t)0, (size_t)(nnz_raw + 1),
-                                             rocprim::plus<int64_t>(), stream));
-        DevBuf<char> tmp;
-        BFSX_HIP_TRY(tmp.alloc(tmp_bytes));
-        BFSX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, in, pos.p, (int64_t)0, (size_t)(nnz_raw + 1),
-                                             rocprim::plus<int64_t>(), stream));
-    }
-    int64_t nnz = 0;
-    BFSX_HIP_TRY(hipMemcpyAsync(&nnz, pos.p + nnz_raw, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
-    BFSX_HIP_TRY(hipStreamSynchronize(stream));
-
-    DevBuf<uint32_t> col_f;
-    DevBuf<int64_t> noff;
-    BFSX_HIP_TRY(col_f.alloc(nnz));
-    BFSX_HIP_TRY(noff.alloc(nv + 1));
-    if (nnz_raw > 0) {
-        hipLaunchKernelGGL(k_compact, dim3(grid_for(nnz_raw, kBS)), dim3(kBS), 0, stream, col_s.p, keep.p, pos.p,
-                           nnz_raw, col_f.p);
-        BFSX_HIP_TRY(hipGetLastError());
-    }
-    hipLaunchKernelGGL(k_new_off, dim3(grid_for(nv + 1, kBS)), dim3(kBS), 0, stream, off.p, pos.p, nv, noff.p);
-    BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipStreamSynchronize(stream));
-    col_s.reset();
-    keep.reset();
-    pos.reset();
+    DevBuf<uint32_t> &col_f = col;
     if (degree_order) {
         DevBuf<uint32_t> gdeg;
         if (partitioned) {

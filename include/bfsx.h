@@ -94,7 +94,11 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
  *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS)
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
- *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU; fixed at a graph's first BFS) */
+ *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU; fixed at a graph's first BFS)
+ *   "hub_bits" = auto|off|1..30 (bottom-up probes of the 2^b highest-degree vertices go to a small
+ *                 gathered bitmap; auto = n/1024 rounded up to a power of two; fixed at a graph's first BFS)
+ *   "build_chunk" = int (CSR build: raw adjacency entries per sort/dedup chunk, default 2^30; bounds the
+ *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */

@@ -300,3 +300,61 @@ def test_repeated_bfs_reuses_state(ctx):
         assert np.array_equal(d, d0)
         d2, p2 = g.result()
         assert np.array_equal(d2, d0)
+
+
+@pytest.mark.parametrize("bits", ["off", "1", "6", "12", "30"])
+@pytest.mark.parametrize("direction", ["auto", "bottomup"])
+def test_hub_probe_domain(ctx, bits, direction):
+    """k_bu's hub-encoded probes (option hub_bits: 2^b highest-degree vertices get a dense second id;
+    30 = every vertex is a hub, 1 = two hubs): distances bit-exact and parents valid whatever the hub
+    count, on edge-case graphs and a scale-14 Kronecker graph."""
+    cases = [c for c in random_cases() if c[0] in ("rand3", "star", "multi_hub", "two_comp", "isolated", "dups")]
+    ctx.set_option("hub_bits", bits)
+    ctx.set_option("direction", direction)
+    try:
+        for name, nv, u, v in cases:
+            u = np.asarray(u, np.uint32)
+            v = np.asarray(v, np.uint32)
+            off, col = O.build_sets(nv, u, v)
+            with ctx.from_edges(nv, u, v) as g:
+                for s in sorted({0, nv - 1, nv // 2}):
+                    check_against_oracle(g, nv, off, col, s, u, v, mr=False)
+                    assert g.validate()["errors"] == 0
+        ou, ov = O.kronecker(14, 16, 0x5EED2026)
+        off, col = O.build_sets(1 << 14, ou, ov)
+        with ctx.kronecker(14, 16, 0x5EED2026) as g:
+            for r in g.sample_roots(3, seed=9):
+                check_against_oracle(g, 1 << 14, off, col, int(r), ou, ov, mr=False)
+    finally:
+        ctx.set_option("hub_bits", "auto")
+        ctx.set_option("direction", "auto")
+
+
+@pytest.mark.parametrize("chunk", ["1", "37", "5000"])
+def test_chunked_csr_build(ctx, chunk):
+    """The CSR build sorts/dedups/orders rows in chunks of `build_chunk` raw entries, compacting in place
+    (what lets scale 30 build on one device).  Tiny chunks (1 = one row per chunk, rows longer than the
+    chunk, chunk edges inside duplicate runs) must give the same neighbour sets and degree order."""
+    cases = [c for c in random_cases() if c[0] in ("rand0", "rand5", "star", "dups", "self_loops", "isolated")]
+    ctx.set_option("build_chunk", chunk)
+    try:
+        for name, nv, u, v in cases:
+            u = np.asarray(u, np.uint32)
+            v = np.asarray(v, np.uint32)
+            off, col = O.build_sets(nv, u, v)
+            with ctx.from_edges(nv, u, v) as g:
+                goff, gcol = g.csr()
+                assert same_sets(off, col, goff, gcol), name
+                # degree-descending order inside every row (ties by id)
+                deg = np.diff(goff)
+                rows = np.repeat(np.arange(nv), deg)
+                key = np.lexsort((gcol, -deg[gcol], rows))
+                assert np.array_equal(gcol[key], gcol), name
+                check_against_oracle(g, nv, off, col, 0, u, v, mr=False)
+        ou, ov = O.kronecker(12, 16, 0x5EED2026)
+        off, col = O.build_sets(1 << 12, ou, ov)
+        with ctx.kronecker(12, 16, 0x5EED2026) as g:
+            goff, gcol = g.csr()
+            assert same_sets(off, col, goff, gcol)
+    finally:
+        ctx.set_option("build_chunk", str(1 << 30))
