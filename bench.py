@@ -40,12 +40,12 @@ def load_module(name, file):
 def level_bytes(ls, nwords):
     """Algorithmic bytes of one level."""
     if ls["direction"] == 2:  # bottom-up: visited word read + next word write, top1 of every live
-        # candidate, the uint32 offset pair of each row walked past top1 (`claims` counts them), the
-        # adjacency entries walked, the packed state word of every vertex found.  Frontier-bit probes
-        # are not counted: the 8 MiB bitmap is cache-resident.
-        walked = max(ls["scanned"] - ls["unvisited_in"], 0)
-        return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 8 * ls["claims"] + 4 * walked
-                + 8 * ls["frontier_out"])
+        # candidate, rest[] (2nd..4th neighbours + degree, 16 B) of every top1 miss, the uint32 offset pair
+        # of each row walked past its first four entries (`claims`), the adjacency entries walked there,
+        # the packed state word of every vertex found.  Frontier-bit probes are not counted: the 8 MiB
+        # bitmap is cache-resident.
+        return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 16 * ls["stage2"] + 8 * ls["claims"]
+                + 4 * ls["walked"] + 8 * ls["frontier_out"])
     # top-down: queue read, row offsets (2 x 8 B per frontier vertex), adjacency rows, winners'
     # dist+parent writes, queue append, degree lookups of the winners
     return 20 * ls["frontier_in"] + 4 * max(ls["mf_in"], 0) + 28 * ls["frontier_out"]

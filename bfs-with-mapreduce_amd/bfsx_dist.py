@@ -142,7 +142,7 @@ class GpuEngine:
 class DistBFS:
     """Level-synchronous partitioned BFS; every rank runs the same loop in lockstep."""
 
-    def __init__(self, engine, comm, direction="auto", alpha=30, beta=24):
+    def __init__(self, engine, comm, direction="auto", alpha=20, beta=24):
         self.e, self.c = engine, comm
         self.direction, self.alpha, self.beta = direction, alpha, beta
         self.nnz_global = comm.allreduce_i64([engine.nnz_local()])[0]

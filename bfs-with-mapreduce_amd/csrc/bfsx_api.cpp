@@ -269,6 +269,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         }
         return as_int(ctx->opt.persist_blocks);
     }
+    if (k == "bu_unroll") {
+        if (v == "2") ctx->opt.bu_unroll = 2;
+        else if (v == "4") ctx->opt.bu_unroll = 4;
+        else return fail(BFSX_E_ARG, "bu_unroll must be 2|4");
+        return BFSX_OK;
+    }
     if (k == "build_chunk") {
         char *end = nullptr;
         const long long x = strtoll(value, &end, 10);

@@ -25,7 +25,8 @@ int fail(int code, const std::string &msg);
 
 struct Options {
     int direction = BFSX_DIR_AUTO;
-    int alpha = 30;             // top-down -> bottom-up when m_f > m_u / alpha (tuned on scale 26)
+    int alpha = 20;             // top-down -> bottom-up when m_f > m_u / alpha (re-tuned on scale 26 with the
+                                // two-stage bottom-up: 20 vs 30 = +2%, within run-to-run noise of 10..45)
     int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
@@ -33,6 +34,7 @@ struct Options {
     int offset_bits = 0;        // traversal row-offset width: 0 = uint32 when nnz < 2^32, else int64; 64 = int64
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
     int hub_bits = -1;          // bottom-up hub probe domain: -1 auto, 0 off, b = 2^b hubs
+    int bu_unroll = 4;          // bottom-up candidates per lane per round (4 or 2)
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
 };
 

@@ -44,10 +44,11 @@ struct alignas(64) StatShard {
     u64 scanned; // adjacency entries read (algorithmic-bytes accounting)
     u64 claims;  // top-down atomicOr claims attempted (diagnostics)
     u64 mu;      // bottom-up: degree sum of the candidates left unvisited (Beamer m_u, exact)
+    u64 stage2;  // bottom-up: candidates that loaded rest[] (stage A2, 16 B each)
+    u64 walked;  // bottom-up: adjacency entries read from col in phase B (4 B each)
     u64 dmax;    // top-down: largest degree in the produced frontier (skips the hub bin when <= hub_deg)
-    u64 pad[2];
 };
-constexpr int kStatFields = 5;
+constexpr int kStatFields = 7; // summed fields, in declaration order (dmax is a max)
 
 // Counters of one level.  Level L reads slot L%3 (its own frontier, already on the host), accumulates
 // the frontier it produces into slot (L+1)%3 and zeroes slot (L+2)%3: no per-level memset.
@@ -70,7 +71,7 @@ struct alignas(64) PersistRec {
 // A level's counter sums as the host reads them (mapped pinned memory, written by k_publish).
 struct alignas(64) Published {
     u64 seq;
-    int64_t qtail, nf, mf, sc, cl, mu, dmax;
+    int64_t qtail, nf, mf, sc, cl, mu, dmax, stage2, walked;
 };
 
 } // namespace
@@ -83,6 +84,7 @@ struct BfsWorkspace {
     u64 *dead = nullptr;                // isolated vertices + padding (initial visited bitmap)
     int64_t n_dead = 0;                 // isolated vertices (excluding padding)
     uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex (+ kDeg1 flag)
+    uint4 *rest = nullptr;              // {2nd, 3rd, 4th neighbour, degree} of every vertex (k_bu stage A2)
     uint32_t top1_flag = 0;             // kDeg1 when every global id < 2^31, else 0 (flag unused)
     // hub-encoded probe domain of the bottom-up kernel (single device; see k_bu): the hub_k highest-degree
     // vertices, their frontier bits gathered into a small bitmap per bottom-up level
@@ -149,8 +151,8 @@ __device__ inline void zero_slot(LevelSlot *ring, int level) {
     }
 }
 
-// Block-uniform: reduce the per-thread stat values over the workgroup; threads 0..4 add them to this
-// workgroup's shard of the level's counters.  Order: nf, mf, scanned, claims, mu.
+// Block-uniform: reduce the per-thread stat values over the workgroup; threads 0..6 add them to this
+// workgroup's shard of the level's counters.  Order: nf, mf, scanned, claims, mu, stage2, walked.
 __device__ inline u64 wave_max(u64 x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -160,12 +162,13 @@ __device__ inline u64 wave_max(u64 x) {
     return x;
 }
 
-__device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu, u64 dmax = 0) {
+__device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu, u64 dmax = 0,
+                                 u64 stage2 = 0, u64 walked = 0) {
     __shared__ u64 s_red[kStatFields][kWaves];
     __shared__ u64 s_dmax[kWaves];
     dmax = wave_max(dmax);
     if (lane_id() == 0) s_dmax[threadIdx.x >> 6] = dmax;
-    u64 v[kStatFields] = {nf, mf, scanned, claims, mu};
+    u64 v[kStatFields] = {nf, mf, scanned, claims, mu, stage2, walked};
     const unsigned wave = threadIdx.x >> 6;
 #pragma unroll
     for (int f = 0; f < kStatFields; f++) {
@@ -213,8 +216,10 @@ __global__ void k_publish(const LevelSlot *__restrict__ slot, Published *pub, u6
     const unsigned lane = threadIdx.x; // one wave, lane i sums shard i
     const StatShard &sh = slot->sh[lane];
     const u64 nf = wave_sum(sh.nf), mf = wave_sum(sh.mf), sc = wave_sum(sh.scanned), cl = wave_sum(sh.claims),
-              mu = wave_sum(sh.mu), dmax = wave_max(sh.dmax);
+              mu = wave_sum(sh.mu), dmax = wave_max(sh.dmax), s2 = wave_sum(sh.stage2), wk = wave_sum(sh.walked);
     if (lane == 0) {
+        pub->stage2 = (int64_t)s2;
+        pub->walked = (int64_t)wk;
         pub->qtail = (int64_t)slot->qtail;
         pub->nf = (int64_t)nf;
         pub->mf = (int64_t)mf;
@@ -929,8 +934,7 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ 
 // and top1 carry kHubBit | h for hub entries, and a kernel before each bottom-up level gathers the
 // hubs' frontier bits into `hfront` (hub_k bits: 256 KiB at scale 26, L2-resident on every XCD).  A
 // hub probe reads hfront, any other probe reads front; the parent of a hub hit is hub_id[h].
-constexpr int kBuU = 4;
-constexpr int kBuRound = 64 * kBuU;
+// kU: candidates per lane per round (4 at 6 waves/SIMD, or 2 at 8 waves/SIMD; option "bu_unroll")
 constexpr uint32_t kDeg1 = 0x80000000u;
 constexpr uint32_t kHubBit = 0x40000000u; // hub encoding needs every global id < 2^30
 constexpr uint32_t kHubMask = kHubBit - 1u;
@@ -949,20 +953,33 @@ __device__ inline uint32_t probe_id(const uint32_t *__restrict__ hub_id, uint32_
     return (kHubs && (x & kHubBit)) ? hub_id[x & kHubMask] : x;
 }
 
-template <class OffT, bool kMf, bool kHubs>
-__global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                            const uint32_t *__restrict__ top1, const u64 *__restrict__ front,
-                                            u64 *__restrict__ next, u64 *__restrict__ vis, u64 *__restrict__ stt,
-                                            LevelSlot *ring, int level, int64_t nwords, uint32_t fmask,
-                                            const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id) {
+// frontier bit of probe id x (32-bit probe word: one VGPR per probe in flight)
+template <bool kHubs>
+__device__ inline uint32_t probe_bit(const u64 *__restrict__ front, const u64 *__restrict__ hfront, uint32_t x) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, x));
+    return (w[(x >> 5) & 1u] >> (x & 31u)) & 1u;
+}
+
+// Second stage of phase A (see below): rest[v] = {c1, c2, c3, deg} -- the 2nd..4th neighbours of v in
+// row order (the last one repeated for rows shorter than 4, so every slot is a real neighbour) and
+// its degree (saturated at 2^32-1).  A miss on top1 probes c1..c3 at once from this one 16-B load;
+// only rows longer than 4 without a hit there walk their row (phase B, from entry 4).
+template <class OffT, bool kMf, bool kHubs, int kU>
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6 : 7))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                            const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
+                                            const u64 *__restrict__ front, u64 *__restrict__ next,
+                                            u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
+                                            int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
+                                            const uint32_t *__restrict__ hub_id) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
-    __shared__ uint32_t s_miss[kWaves][kBuRound];
+    __shared__ uint32_t s_miss[kWaves][(64 * kU)];
     __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
-    u64 acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0;
+    // per-lane counters fit 32 bits (a lane sees a few hundred candidates per launch); widened at the end
+    uint32_t acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0;
     const int64_t wstride = (int64_t)gridDim.x * kWaves * 64;
     for (int64_t w0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; w0 < nwords; w0 += wstride) {
         const int64_t wl = w0 + lane;
@@ -980,7 +997,7 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
         __builtin_amdgcn_wave_barrier();
         const uint32_t vbase = (uint32_t)(w0 * 64);
         // the group's candidates, one half (32 words, <= 2048 vertices) at a time: each word's lane
-        // writes the offsets of its unvisited bits at its rank, then rounds of kBuRound candidates
+        // writes the offsets of its unvisited bits at its rank, then rounds of (64 * kU) candidates
         const uint32_t half = __shfl(incl, 31); // candidates in words 0..31
         for (int h = 0; h < 2; h++) {
             const uint32_t hb = h ? half : 0u, he = h ? total : half;
@@ -994,59 +1011,95 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
                 }
             }
             __builtin_amdgcn_wave_barrier();
-            for (uint32_t t0 = hb; t0 < he; t0 += kBuRound) {
-                uint32_t v[kBuU], x[kBuU];
-                u64 fw[kBuU];
+            for (uint32_t t0 = hb; t0 < he; t0 += (64 * kU)) {
+                uint32_t v[kU], x[kU];
 #pragma unroll
-                for (int k = 0; k < kBuU; k++) // past the half's end: masked below
+                for (int k = 0; k < kU; k++) // past the half's end: masked below
                     v[k] = vbase + s_cand[wave][t0 - hb + (uint32_t)k * 64 + lane];
                 __builtin_amdgcn_wave_barrier();
+                // A1: top1 of every candidate, then its frontier bit
 #pragma unroll
-                for (int k = 0; k < kBuU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < he) ? top1[v[k]] : 0u;
+                for (int k = 0; k < kU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < he) ? top1[v[k]] : 0u;
+                uint32_t fbm = 0u; // bit k: candidate k's top1 is in the frontier
 #pragma unroll
-                for (int k = 0; k < kBuU; k++) {
-                    const uint32_t id = x[k] & ~fmask;
-                    fw[k] = (t0 + (uint32_t)k * 64 + lane < he) ? *probe_word<kHubs>(front, hfront, id) : 0ull;
+                for (int k = 0; k < kU; k++)
+                    fbm |= ((t0 + (uint32_t)k * 64 + lane < he) ? probe_bit<kHubs>(front, hfront, x[k] & ~fmask) : 0u)
+                           << k;
+                // A2: misses of A1 load rest[v] (c1..c3 + degree) and probe c1..c3 together
+                uint4 r[kU];
+#pragma unroll
+                for (int k = 0; k < kU; k++) {
+                    const bool a2 = (t0 + (uint32_t)k * 64 + lane < he) && !((fbm >> k) & 1u) && !(x[k] & fmask);
+                    r[k] = a2 ? rest[v[k]] : make_uint4(0u, 0u, 0u, 0u);
+                    acc_s2 += a2;
+                }
+                uint32_t pbm = 0u; // bits 3k..3k+2: c1..c3 of candidate k in the frontier
+#pragma unroll
+                for (int k = 0; k < kU; k++) {
+                    if (r[k].w != 0u) {
+                        pbm |= (probe_bit<kHubs>(front, hfront, r[k].x) | (probe_bit<kHubs>(front, hfront, r[k].y) << 1) |
+                                (probe_bit<kHubs>(front, hfront, r[k].z) << 2))
+                               << (3 * k);
+                    }
                 }
                 uint32_t nmiss = 0; // wave-uniform
 #pragma unroll
-                for (int k = 0; k < kBuU; k++) {
+                for (int k = 0; k < kU; k++) {
                     const bool ok = t0 + (uint32_t)k * 64 + lane < he;
-                    const uint32_t id = x[k] & ~fmask;
-                    const bool hit = ok && ((fw[k] >> (id & 63u)) & 1ull);
-                    const bool last = (x[k] & fmask) != 0; // top1 was the row's only entry
-                    if (ok) acc_sc += 1;
-                    if (hit) {
-                        stt[v[k]] = pack_state(probe_id<kHubs>(hub_id, id), nd);
+                    const bool deg1 = (x[k] & fmask) != 0; // top1 was the row's only entry
+                    const uint32_t deg = r[k].w;           // 0 unless A2 ran
+                    bool found = false, miss = false;
+                    uint32_t par = 0;
+                    const uint32_t pb = (pbm >> (3 * k)) & 7u;
+                    if (ok) {
+                        if ((fbm >> k) & 1u) {
+                            found = true;
+                            par = x[k] & ~fmask;
+                            acc_sc += 1;
+                        } else if (deg1) {
+                            acc_mu += 1;
+                            acc_sc += 1;
+                        } else if (pb) {
+                            found = true;
+                            par = (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z;
+                            acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
+                        } else if (deg <= 4u) {
+                            acc_mu += deg;
+                            acc_sc += deg;
+                        } else {
+                            miss = true;
+                            acc_sc += 4;
+                        }
+                    }
+                    if (found) {
+                        stt[v[k]] = pack_state(probe_id<kHubs>(hub_id, par), nd);
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
-                        if (kMf) acc_mf += (u64)(row_off[v[k] + 1] - row_off[v[k]]);
-                    } else if (ok && last) {
-                        acc_mu += 1;
+                        if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
                     }
-                    const bool miss = ok && !hit && !last;
                     const u64 mm = __ballot(miss);
                     if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
                     nmiss += (uint32_t)__popcll(mm);
                 }
                 __builtin_amdgcn_wave_barrier();
+                // B: rows longer than 4 with no hit in their first 4 entries walk the rest, 4 per step
                 for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
                     if (m0 + lane < nmiss) {
                         const uint32_t vv = s_miss[wave][m0 + lane];
                         const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
                         bool found = false;
                         uint32_t par = 0;
-                        int64_t j = b + 1;
+                        int64_t j = b + 4;
                         while (!found && j < e) {
                             const int64_t left = e - j;
                             const uint32_t x0 = col[j];
                             const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                             const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                             const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                            const bool h0 = (*probe_word<kHubs>(front, hfront, x0) >> (x0 & 63u)) & 1ull;
-                            const bool h1 = (*probe_word<kHubs>(front, hfront, x1) >> (x1 & 63u)) & 1ull;
-                            const bool h2 = (*probe_word<kHubs>(front, hfront, x2) >> (x2 & 63u)) & 1ull;
-                            const bool h3 = (*probe_word<kHubs>(front, hfront, x3) >> (x3 & 63u)) & 1ull;
+                            const uint32_t h0 = probe_bit<kHubs>(front, hfront, x0);
+                            const uint32_t h1 = probe_bit<kHubs>(front, hfront, x1);
+                            const uint32_t h2 = probe_bit<kHubs>(front, hfront, x2);
+                            const uint32_t h3 = probe_bit<kHubs>(front, hfront, x3);
                             if (h0 | h1 | h2 | h3) {
                                 found = true;
                                 const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
@@ -1056,15 +1109,16 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
                                 j += left < 4 ? left : 4;
                             }
                         }
-                        acc_sc += (u64)(j - b - 1);
+                        acc_sc += (uint32_t)(j - b - 4);
+                        acc_wk += (uint32_t)(j - b - 4);
                         acc_rows += 1;
                         if (found) {
                             stt[vv] = pack_state(probe_id<kHubs>(hub_id, par), nd);
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
-                            if (kMf) acc_mf += (u64)(e - b);
+                            if (kMf) acc_mf += (uint32_t)(e - b);
                         } else {
-                            acc_mu += (u64)(e - b);
+                            acc_mu += (uint32_t)(e - b);
                         }
                     }
                 }
@@ -1078,7 +1132,8 @@ __global__ __launch_bounds__(kBS) void k_bu(const OffT *__restrict__ row_off, co
             if (nxl) vis[wl] = vwl | nxl;
         }
     }
-    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu); // claims field: rows walked (phase B)
+    // claims field: rows walked (phase B)
+    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk);
 }
 
 // ---- K4: frontier representation changes -------------------------------------------------------
@@ -1202,6 +1257,23 @@ __global__ __launch_bounds__(kBS) void k_top1(const int64_t *__restrict__ row_of
     }
 }
 
+// rest[v] = {c1, c2, c3, deg} of row v (see k_bu); rows shorter than 4 repeat their last entry
+// (a degree-1 row repeats top1: probing it again is harmless).
+__global__ __launch_bounds__(kBS) void k_rest(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                              int64_t nv, uint4 *__restrict__ rest) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
+        const int64_t b = row_off[v], d = row_off[v + 1] - b;
+        uint4 r = make_uint4(0u, 0u, 0u, 0u);
+        if (d > 0) {
+            r.x = col[b + (d > 1 ? 1 : d - 1)];
+            r.y = col[b + (d > 2 ? 2 : d - 1)];
+            r.z = col[b + (d > 3 ? 3 : d - 1)];
+            r.w = d >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)d;
+        }
+        rest[v] = r;
+    }
+}
+
 // Hub selection: sort keys ~degree (ascending = degree descending, ties by id: the sort is stable).
 __global__ __launch_bounds__(kBS) void k_hub_keys(const int64_t *__restrict__ row_off, int64_t nv,
                                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
@@ -1272,7 +1344,7 @@ __global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, cons
 }
 
 // Multi-GPU level close: one workgroup sums the level's counter shards into
-//   out[0..4] = local {n_f, m_f, m_u, scanned, rows/claims}   out[8..10] = copy of {n_f, m_f, m_u}
+//   out[0..6] = local {n_f, m_f, m_u, scanned, rows/claims, stage2, walked}   out[8..10] = copy of {n_f, m_f, m_u}
 // (the copy is all-reduced in place; the local half stays for the per-level record).
 __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out) {
     __shared__ u64 s[kStatFields][kShards];
@@ -1282,6 +1354,8 @@ __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, in
         s[2][i] = slot->sh[i].mu;
         s[3][i] = slot->sh[i].scanned;
         s[4][i] = slot->sh[i].claims;
+        s[5][i] = slot->sh[i].stage2;
+        s[6][i] = slot->sh[i].walked;
     }
     __syncthreads();
     if (threadIdx.x < kStatFields) {
@@ -1402,6 +1476,10 @@ int ws_alloc(bfsx_graph *g) {
     hipLaunchKernelGGL(k_top1, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->d_col, g->nv, ws->top1_flag, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
     if (int e = hub_setup(g, ws)) return e;
+    BFSX_HIP_TRY(hipMalloc(&ws->rest, nv * sizeof(uint4)));
+    hipLaunchKernelGGL(k_rest, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, ws->hub_k > 0 ? ws->colh : g->d_col,
+                       g->nv, ws->rest);
+    BFSX_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
                        g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
     BFSX_HIP_TRY(hipGetLastError());
@@ -1452,14 +1530,14 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     return BFSX_OK;
 }
 
-template <class OffT, bool kMf, bool kHubs>
-int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
+template <class OffT, bool kMf, bool kHubs, int kU>
+int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
     hipStream_t st = g->ctx->stream;
     // persistent grid: exactly the resident workgroups (a partial second wave of workgroups would
     // leave most CUs idle at the tail of the grid-stride loop)
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs>, kBS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs, kU>, kBS, 0) != hipSuccess ||
             per_cu < 1)
             per_cu = 4;
     }
@@ -1470,11 +1548,18 @@ int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
                            ws->hub_id, ws->hub_k, front, ws->hfront);
         BFSX_HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
-                       ws->top1, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag,
+    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
+                       ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
+                       ws->top1_flag,
                        ws->hfront, ws->hub_id);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
+}
+
+template <class OffT, bool kMf, bool kHubs>
+int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
+    return g->ctx->opt.bu_unroll == 2 ? launch_bu_u<OffT, kMf, kHubs, 2>(g, ws, row_off, front, level)
+                                      : launch_bu_u<OffT, kMf, kHubs, 4>(g, ws, row_off, front, level);
 }
 
 template <bool kMf>
@@ -1487,7 +1572,7 @@ int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
 }
 
 struct SlotSums {
-    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0;
+    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0;
 };
 
 // Spin until k_publish of the current sequence number has landed; poll the stream now and then so a
@@ -1514,6 +1599,8 @@ SlotSums sum_slot(const LevelSlot *s) {
         r.sc += (int64_t)s->sh[i].scanned;
         r.cl += (int64_t)s->sh[i].claims;
         r.mu += (int64_t)s->sh[i].mu;
+        r.s2 += (int64_t)s->sh[i].stage2;
+        r.wk += (int64_t)s->sh[i].walked;
     }
     return r;
 }
@@ -1615,7 +1702,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->persist_brec, ws->persist_ctl})
         if (p) (void)hipFree(p);
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
-                    (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1,
+                    (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr})
         if (p) (void)hipFree(p);
@@ -1762,6 +1849,8 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         s.sc = ws->h_pub->sc;
         s.cl = ws->h_pub->cl;
         s.mu = ws->h_pub->mu;
+        s.s2 = ws->h_pub->stage2;
+        s.wk = ws->h_pub->walked;
         const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? ws->h_pub->qtail : s.nf;
         g->level_dirs.push_back(dir);
         bfsx_level_stat ls{};
@@ -1773,6 +1862,8 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         ls.unvisited_in = nv - visited - ws->n_dead;      // live candidates (isolated ones are pre-visited)
         ls.scanned = s.sc;
         ls.claims = s.cl;
+        ls.stage2 = s.s2;
+        ls.walked = s.wk;
         g->level_stats.push_back(ls);
         timing.push_back({level, false, 0.0, 0.0});
         examined += ls.scanned;
@@ -2063,6 +2154,8 @@ int dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local) {
     ls.mf_in = ws->d_mf;
     ls.scanned = s.sc;
     ls.claims = s.cl;
+    ls.stage2 = s.s2;
+    ls.walked = s.wk;
     g->level_stats.push_back(ls);
     g->level_dirs.push_back(ws->d_dir);
     if (td) std::swap(ws->qa, ws->qb);
@@ -2286,6 +2379,8 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         ls.unvisited_in = g->nv - visited_local - ws->n_dead;
         ls.scanned = h[3];
         ls.claims = h[4];
+        ls.stage2 = h[5];
+        ls.walked = h[6];
         g->level_stats.push_back(ls);
         g->level_dirs.push_back(dir);
         examined += h[3];

@@ -78,6 +78,8 @@ typedef struct bfsx_level_stat {
     int64_t claims;        /* top-down: atomic visited-bitmap claims attempted; bottom-up: rows walked past top1 */
     double kernel_ms;      /* device time of this level's kernels (hipEvents around them) */
     double cum_ms;         /* device time since source init, like the reference's Stopwatch */
+    int64_t stage2;        /* bottom-up: candidates that read their 2nd..4th neighbours (16-B rest[] load) */
+    int64_t walked;        /* bottom-up: adjacency entries read from the CSR past the first four (phase B) */
 } bfsx_level_stat;
 
 /* ---- library / context ---------------------------------------------------------------------- */
@@ -87,7 +89,7 @@ const char *bfsx_last_error(void);
 int bfsx_init(int device, bfsx_ctx **out);
 void bfsx_finalize(bfsx_ctx *ctx);
 /* Options (all optional; defaults preserve reference behaviour):
- *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 30) ; "beta" = int (default 24)
+ *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 20) ; "beta" = int (default 24)
  *   "hub_degree" = int (top-down multi-workgroup bin threshold, default 64)
  *   "row_order" = degree|id (adjacency order inside a CSR row for graphs built afterwards; default
  *                 degree = high-degree neighbours first, which shortens bottom-up probes)

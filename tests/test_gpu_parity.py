@@ -358,3 +358,29 @@ def test_chunked_csr_build(ctx, chunk):
             assert same_sets(off, col, goff, gcol)
     finally:
         ctx.set_option("build_chunk", str(1 << 30))
+
+
+@pytest.mark.parametrize("unroll", ["2", "4"])
+def test_bottomup_unroll_variants(ctx, unroll):
+    """Both k_bu instantiations (2 or 4 candidates per lane per round) are bit-exact, pull-only and
+    direction-optimising, with and without the hub probe domain."""
+    ctx.set_option("bu_unroll", unroll)
+    try:
+        for hub in ("off", "auto"):
+            ctx.set_option("hub_bits", hub)
+            for direction in ("bottomup", "auto"):
+                ctx.set_option("direction", direction)
+                for name, nv, u, v in [c for c in random_cases() if c[0] in ("rand2", "multi_hub", "path")]:
+                    u = np.asarray(u, np.uint32)
+                    v = np.asarray(v, np.uint32)
+                    off, col = O.build_sets(nv, u, v)
+                    with ctx.from_edges(nv, u, v) as g:
+                        check_against_oracle(g, nv, off, col, 0, u, v, mr=False)
+                ou, ov = O.kronecker(16, 16, 0x5EED2026)
+                off, col = O.build_sets(1 << 16, ou, ov)
+                with ctx.kronecker(16, 16, 0x5EED2026) as g:
+                    for r in g.sample_roots(2, seed=4):
+                        check_against_oracle(g, 1 << 16, off, col, int(r), ou, ov, mr=False)
+    finally:
+        for k, val in (("bu_unroll", "4"), ("hub_bits", "auto"), ("direction", "auto")):
+            ctx.set_option(k, val)
