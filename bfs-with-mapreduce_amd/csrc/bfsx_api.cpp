@@ -269,6 +269,13 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         }
         return as_int(ctx->opt.persist_blocks);
     }
+    if (k == "hybrid") {
+        if (v == "off") ctx->opt.hybrid = 0;
+        else if (v == "auto") ctx->opt.hybrid = 1;
+        else if (v == "force") ctx->opt.hybrid = 2;
+        else return fail(BFSX_E_ARG, "hybrid must be auto|off|force");
+        return BFSX_OK;
+    }
     if (k == "bu_unroll") {
         if (v == "2") ctx->opt.bu_unroll = 2;
         else if (v == "4") ctx->opt.bu_unroll = 4;

@@ -65,8 +65,9 @@ constexpr uint32_t kPersistNf = 8192; // widest frontier a K3p level may produce
 constexpr int kPersistLevels = 1024;  // levels per launch
 
 struct alignas(64) PersistRec {
-    u64 qtail, mf, dmax, scanned, claims, t_end, pad[2];
+    u64 qtail, mf, dmax, scanned, claims, t_end, mfh, pad; // mfh: degree sum of the hubs discovered
 };
+constexpr int kRecWords = 5; // per-workgroup record words of a K3p level
 
 // A level's counter sums as the host reads them (mapped pinned memory, written by k_publish).
 struct alignas(64) Published {
@@ -90,6 +91,7 @@ struct BfsWorkspace {
     // vertices, their frontier bits gathered into a small bitmap per bottom-up level
     int64_t hub_k = 0;                  // 0: off
     uint32_t *hub_id = nullptr;         // [hub_k] global id of hub h (degree descending)
+    uint32_t hub_tdeg = 0xFFFFFFFFu;    // the hubs are exactly the vertices of degree >= hub_tdeg
     uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
     u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
@@ -343,7 +345,8 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
                                       int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, u64 *qtail,
-                                      const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax) {
+                                      const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
+                                      uint32_t t_hub, u64 &acc_mfh, u64 &acc_nh) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -378,6 +381,10 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
                 acc_mf += dg;
                 acc_dmax = dg > acc_dmax ? dg : acc_dmax;
+                if (dg >= t_hub) { // a hub of the bottom-up hub domain (hybrid levels, bfs_run)
+                    acc_mfh += dg;
+                    acc_nh += 1;
+                }
             }
             bq_push(q, win, vl);
             if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
@@ -393,7 +400,8 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
                                             LevelSlot *ring, int level, uint32_t hub_deg,
-                                            uint32_t *__restrict__ hubs, Part pt, int gsz) {
+                                            uint32_t *__restrict__ hubs, Part pt, int gsz, uint32_t t_hub,
+                                            uint32_t skip_deg) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
@@ -407,7 +415,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     if (kDist && threadIdx.x == 0) rq->n = 0;
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0;
     // gsz (<= kBS) frontier vertices per workgroup and step: a narrow frontier spreads over more
     // workgroups, so each sweeps its rows in one step instead of several dependent ones
     for (uint32_t base = blockIdx.x * gsz; base < qlen; base += gridDim.x * gsz) {
@@ -418,7 +426,9 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             u = qin[i];
             beg = (int64_t)row_off[u];
             int64_t d = (int64_t)row_off[u + 1] - beg;
-            if (d > (int64_t)hub_deg) {
+            if (d >= (int64_t)skip_deg) { // hybrid level: the bottom-up hub sweep covers this vertex
+                d = 0;
+            } else if (d > (int64_t)hub_deg) {
                 hubs[atomicAdd(&cn->nhub, 1ull)] = u;
                 d = 0;
             }
@@ -443,19 +453,20 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
         }
         __syncthreads();
         sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt, rq,
-                              acc_mf, attempts, acc_dmax);
+                              acc_mf, attempts, acc_dmax, t_hub, acc_mfh, acc_nh);
         __syncthreads();
     }
     bq_flush(q, qout, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax);
+    // top-down: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
 }
 
 template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  u64 *vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
-                                                 Part pt) {
+                                                 Part pt, uint32_t t_hub) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
@@ -470,7 +481,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x;
     constexpr int kPer = kHubBatch / kBS;
-    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0;
     __syncthreads();
     for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
         const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
@@ -512,12 +523,12 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
         sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt,
-                              rq, acc_mf, attempts, acc_dmax);
+                              rq, acc_mf, attempts, acc_dmax, t_hub, acc_mfh, acc_nh);
         __syncthreads();
     }
     bq_flush(q, qout, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
 }
 
 // ---- K3p: persistent top-down for narrow frontiers --------------------------------------------------
@@ -601,7 +612,7 @@ __device__ inline bool grid_sync(PersistCtl *ctl, u64 round) {
 }
 
 // alpha <= 0: no direction switch (direction forced top-down).  q0: the first level's frontier
-// (contiguous); seg: 2 parities x G segments of kRegion; brec: 2 parities x G records (4 words);
+// (contiguous); seg: 2 parities x G segments of kRegion; brec: 2 parities x G records (kRecWords);
 // qfinal: the last frontier, contiguous.  bar0: barrier rounds completed by earlier launches.
 template <class OffT>
 __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
@@ -609,14 +620,14 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
-                                                    PersistOut *out) {
+                                                    PersistOut *out, uint32_t t_hub) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_scan[kBS + 1];
     __shared__ int64_t s_beg[kBS];
     __shared__ uint32_t s_u[kBS];
     __shared__ uint32_t s_wsum[kWaves];
-    __shared__ u64 s_red[4][kWaves];
+    __shared__ u64 s_red[5][kWaves];
     __shared__ uint32_t s_n;
     (void)s_dyn;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
@@ -632,10 +643,10 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
     for (int it = 0;; it++) {
         const uint32_t *sin = seg + (size_t)((it + 1) & 1) * G * kRegion; // previous level's segments
         uint32_t *sout = seg + (size_t)(it & 1) * G * kRegion + (size_t)b * kRegion;
-        u64 *rout = brec + (size_t)(it & 1) * G * 4;
+        u64 *rout = brec + (size_t)(it & 1) * G * kRecWords;
         const int32_t nd = level0 + it + 1;
         if (tid == 0) s_n = 0;
-        u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0;
+        u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0;
         const uint32_t vb = (uint32_t)((u64)nf * b / G), ve = (uint32_t)((u64)nf * (b + 1) / G);
         __syncthreads();
         for (uint32_t base = vb; base < ve; base += kBS) {
@@ -715,6 +726,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                         const u64 dg = (u64)(r1[k] - r0[k]);
                         acc_mf += dg;
                         acc_dmax = dg > acc_dmax ? dg : acc_dmax;
+                        acc_mfh += dg >= t_hub ? dg : 0ull;
                     }
                     const u64 mask = __ballot(win);
                     if (mask) {
@@ -733,26 +745,30 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
         }
         // this workgroup's level record
         {
-            const u64 v0 = wave_sum(acc_mf), v1 = wave_sum(scanned), v2 = wave_sum(attempts), v3 = wave_max(acc_dmax);
+            const u64 v0 = wave_sum(acc_mf), v1 = wave_sum(scanned), v2 = wave_sum(attempts), v3 = wave_max(acc_dmax),
+                      v4 = wave_sum(acc_mfh);
             if (lane == 0) {
                 s_red[0][wave] = v0;
                 s_red[1][wave] = v1;
                 s_red[2][wave] = v2;
                 s_red[3][wave] = v3;
+                s_red[4][wave] = v4;
             }
             __syncthreads();
             if (tid == 0) {
-                u64 a = 0, c = 0, d = 0, m = 0;
+                u64 a = 0, c = 0, d = 0, m = 0, h = 0;
                 for (int w = 0; w < kWaves; w++) {
                     a += s_red[0][w];
                     c += s_red[1][w];
                     d += s_red[2][w];
                     m = s_red[3][w] > m ? s_red[3][w] : m;
+                    h += s_red[4][w];
                 }
-                st_sc1(rout + 4 * b + 0, (u64)s_n | (m << 32));
-                st_sc1(rout + 4 * b + 1, a);
-                st_sc1(rout + 4 * b + 2, c);
-                st_sc1(rout + 4 * b + 3, d);
+                st_sc1(rout + kRecWords * b + 0, (u64)s_n | (m << 32));
+                st_sc1(rout + kRecWords * b + 1, a);
+                st_sc1(rout + kRecWords * b + 2, c);
+                st_sc1(rout + kRecWords * b + 3, d);
+                st_sc1(rout + kRecWords * b + 4, h);
             }
         }
         if (!grid_sync(ctl, bar0 + (u64)it + 1)) {
@@ -763,17 +779,19 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             return;
         }
         // every workgroup: the G records -> segment offsets and the level's sums
-        u64 r_n = 0, r_dm = 0, r_mf = 0, r_sc = 0, r_cl = 0;
+        u64 r_n = 0, r_dm = 0, r_mf = 0, r_sc = 0, r_cl = 0, r_mfh = 0;
         if (tid < G) {
-            const u64 w0 = ld_sc1(rout + 4 * tid);
+            const u64 w0 = ld_sc1(rout + kRecWords * tid);
             r_n = w0 & 0xFFFFFFFFull;
             r_dm = w0 >> 32;
-            r_mf = ld_sc1(rout + 4 * tid + 1);
-            r_sc = ld_sc1(rout + 4 * tid + 2);
-            r_cl = ld_sc1(rout + 4 * tid + 3);
+            r_mf = ld_sc1(rout + kRecWords * tid + 1);
+            r_sc = ld_sc1(rout + kRecWords * tid + 2);
+            r_cl = ld_sc1(rout + kRecWords * tid + 3);
+            r_mfh = ld_sc1(rout + kRecWords * tid + 4);
         }
         const uint32_t inc = wave_incl_scan((uint32_t)r_n);
-        const u64 smf = wave_sum(r_mf), ssc = wave_sum(r_sc), scl = wave_sum(r_cl), sdm = wave_max(r_dm);
+        const u64 smf = wave_sum(r_mf), ssc = wave_sum(r_sc), scl = wave_sum(r_cl), sdm = wave_max(r_dm),
+                  smfh = wave_sum(r_mfh);
         __syncthreads(); // s_red / s_wsum reuse
         if (lane == 63) s_wsum[wave] = inc;
         if (lane == 0) {
@@ -781,10 +799,11 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             s_red[1][wave] = ssc;
             s_red[2][wave] = scl;
             s_red[3][wave] = sdm;
+            s_red[4][wave] = smfh;
         }
         __syncthreads();
         uint32_t woff = 0, nf_new = 0;
-        u64 mf_new = 0, sc_new = 0, cl_new = 0, dm_new = 0;
+        u64 mf_new = 0, sc_new = 0, cl_new = 0, dm_new = 0, mfh_new = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; w++) {
             woff += (w < (int)wave) ? s_wsum[w] : 0u;
@@ -793,6 +812,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             sc_new += s_red[1][w];
             cl_new += s_red[2][w];
             dm_new = s_red[3][w] > dm_new ? s_red[3][w] : dm_new;
+            mfh_new += s_red[4][w];
         }
         const uint32_t my_n = (uint32_t)r_n;
         s_off[tid] = woff + inc - my_n; // entries past G: unused
@@ -804,6 +824,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             r.dmax = dm_new;
             r.scanned = sc_new;
             r.claims = cl_new;
+            r.mfh = mfh_new;
             r.t_end = (u64)wall_clock64();
             out->levels = (u64)(it + 1);
         }
@@ -960,11 +981,19 @@ __device__ inline uint32_t probe_bit(const u64 *__restrict__ front, const u64 *_
     return (w[(x >> 5) & 1u] >> (x & 31u)) & 1u;
 }
 
+// Hub sweep (hybrid levels): only hub entries are probed; a non-hub entry reads as "not in frontier"
+// without a memory access (the frontier's non-hub vertices are expanded top-down in the same level).
+template <bool kHubs, bool kHubOnly>
+__device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *__restrict__ hfront, uint32_t x) {
+    if (kHubOnly && !(x & kHubBit)) return 0u;
+    return probe_bit<kHubs>(front, hfront, x);
+}
+
 // Second stage of phase A (see below): rest[v] = {c1, c2, c3, deg} -- the 2nd..4th neighbours of v in
 // row order (the last one repeated for rows shorter than 4, so every slot is a real neighbour) and
 // its degree (saturated at 2^32-1).  A miss on top1 probes c1..c3 at once from this one 16-B load;
 // only rows longer than 4 without a hit there walk their row (phase B, from entry 4).
-template <class OffT, bool kMf, bool kHubs, int kU>
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6 : 7))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
@@ -1023,13 +1052,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                 uint32_t fbm = 0u; // bit k: candidate k's top1 is in the frontier
 #pragma unroll
                 for (int k = 0; k < kU; k++)
-                    fbm |= ((t0 + (uint32_t)k * 64 + lane < he) ? probe_bit<kHubs>(front, hfront, x[k] & ~fmask) : 0u)
+                    fbm |= ((t0 + (uint32_t)k * 64 + lane < he) && (!kHubOnly || (x[k] & kHubBit))
+                                ? probe_bit<kHubs>(front, hfront, x[k] & ~fmask)
+                                : 0u)
                            << k;
                 // A2: misses of A1 load rest[v] (c1..c3 + degree) and probe c1..c3 together
                 uint4 r[kU];
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
-                    const bool a2 = (t0 + (uint32_t)k * 64 + lane < he) && !((fbm >> k) & 1u) && !(x[k] & fmask);
+                    const bool a2 = (t0 + (uint32_t)k * 64 + lane < he) && !((fbm >> k) & 1u) && !(x[k] & fmask) &&
+                                    (!kHubOnly || (x[k] & kHubBit));
                     r[k] = a2 ? rest[v[k]] : make_uint4(0u, 0u, 0u, 0u);
                     acc_s2 += a2;
                 }
@@ -1037,8 +1069,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
                     if (r[k].w != 0u) {
-                        pbm |= (probe_bit<kHubs>(front, hfront, r[k].x) | (probe_bit<kHubs>(front, hfront, r[k].y) << 1) |
-                                (probe_bit<kHubs>(front, hfront, r[k].z) << 2))
+                        pbm |= (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].x) |
+                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].y) << 1) |
+                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].z) << 2))
                                << (3 * k);
                     }
                 }
@@ -1059,13 +1092,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                         } else if (deg1) {
                             acc_mu += 1;
                             acc_sc += 1;
+                        } else if (kHubOnly && !(x[k] & kHubBit)) {
+                            acc_mu += 1; // no hub in the row (degree unknown here; the next pull level recounts m_u)
+                            acc_sc += 1;
                         } else if (pb) {
                             found = true;
                             par = (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z;
                             acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
-                        } else if (deg <= 4u) {
-                            acc_mu += deg;
-                            acc_sc += deg;
+                        } else if (deg <= 4u || (kHubOnly && !(r[k].x & r[k].y & r[k].z & kHubBit))) {
+                            acc_mu += deg; // row exhausted (or, hub sweep: its hub prefix is)
+                            acc_sc += deg < 4u ? deg : 4u;
                         } else {
                             miss = true;
                             acc_sc += 4;
@@ -1087,19 +1123,19 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                     if (m0 + lane < nmiss) {
                         const uint32_t vv = s_miss[wave][m0 + lane];
                         const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
-                        bool found = false;
+                        bool found = false, stop = false;
                         uint32_t par = 0;
                         int64_t j = b + 4;
-                        while (!found && j < e) {
+                        while (!found && !stop && j < e) {
                             const int64_t left = e - j;
                             const uint32_t x0 = col[j];
                             const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                             const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                             const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                            const uint32_t h0 = probe_bit<kHubs>(front, hfront, x0);
-                            const uint32_t h1 = probe_bit<kHubs>(front, hfront, x1);
-                            const uint32_t h2 = probe_bit<kHubs>(front, hfront, x2);
-                            const uint32_t h3 = probe_bit<kHubs>(front, hfront, x3);
+                            const uint32_t h0 = probe_hub<kHubs, kHubOnly>(front, hfront, x0);
+                            const uint32_t h1 = probe_hub<kHubs, kHubOnly>(front, hfront, x1);
+                            const uint32_t h2 = probe_hub<kHubs, kHubOnly>(front, hfront, x2);
+                            const uint32_t h3 = probe_hub<kHubs, kHubOnly>(front, hfront, x3);
                             if (h0 | h1 | h2 | h3) {
                                 found = true;
                                 const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
@@ -1107,6 +1143,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                                 j += h + 1;
                             } else {
                                 j += left < 4 ? left : 4;
+                                // hub sweep: rows are degree-ordered, so past the first non-hub entry no
+                                // hub follows
+                                if (kHubOnly) stop = !(x0 & x1 & x2 & x3 & kHubBit);
                             }
                         }
                         acc_sc += (uint32_t)(j - b - 4);
@@ -1139,6 +1178,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
 // ---- K4: frontier representation changes -------------------------------------------------------
 __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restrict__ q, uint32_t qlen, u64 *bm) {
     for (uint32_t i = blockIdx.x * kBS + threadIdx.x; i < qlen; i += gridDim.x * kBS) {
+        const uint32_t v = q[i];
+        atomicOr(bm + (v >> 6), 1ull << (v & 63u));
+    }
+}
+
+// The same with the queue length read on the device (the top-down half of a hybrid level appends to
+// the queue; its length is known to the host only after the level is published).
+__global__ __launch_bounds__(kBS) void k_queue_to_bitmap_dev(const uint32_t *__restrict__ q, const u64 *qlen, u64 *bm) {
+    const uint32_t n = (uint32_t)*qlen;
+    for (uint32_t i = blockIdx.x * kBS + threadIdx.x; i < n; i += gridDim.x * kBS) {
         const uint32_t v = q[i];
         atomicOr(bm + (v >> 6), 1ull << (v & 63u));
     }
@@ -1282,6 +1331,12 @@ __global__ __launch_bounds__(kBS) void k_hub_keys(const int64_t *__restrict__ ro
         ids[v] = (uint32_t)v;
     }
 }
+__global__ __launch_bounds__(kBS) void k_count_le(const uint32_t *__restrict__ keys, int64_t n, uint32_t x, u64 *out) {
+    u64 c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) c += keys[i] <= x;
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(out, c);
+}
 __global__ __launch_bounds__(kBS) void k_hub_index(const uint32_t *__restrict__ hub_id, int64_t k,
                                                    uint32_t *__restrict__ hidx) {
     for (int64_t h = (int64_t)blockIdx.x * kBS + threadIdx.x; h < k; h += (int64_t)gridDim.x * kBS)
@@ -1415,6 +1470,19 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     BFSX_HIP_TRY(hipMalloc(&sort_tmp.p, std::max<size_t>(tb, 16)));
     BFSX_HIP_TRY(rocprim::radix_sort_pairs(sort_tmp.p, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
                                            (uint32_t *)ids2.p, nv, 0, 32, st));
+    // the hub set is closed under degree ties: every vertex of degree >= the k-th largest degree (so a
+    // kernel tells a hub by its degree alone, and degree-ordered rows hold their hubs as a prefix)
+    uint32_t kth = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&kth, (uint32_t *)keys2.p + (k - 1), sizeof(kth), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
+    hipLaunchKernelGGL(k_count_le, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)keys2.p, g->nv, kth, ws->d_red);
+    BFSX_HIP_TRY(hipGetLastError());
+    u64 keff = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&keff, ws->d_red, sizeof(keff), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    k = (int64_t)keff;
+    ws->hub_tdeg = ~kth;
     BFSX_HIP_TRY(hipMalloc(&ws->hub_id, (size_t)k * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMemcpyAsync(ws->hub_id, ids2.p, (size_t)k * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     BFSX_HIP_TRY(hipMalloc(&hidx.p, nv * sizeof(uint32_t)));
@@ -1497,9 +1565,13 @@ int ws_alloc(bfsx_graph *g) {
 // ---- launch helpers: one per traversal kernel, dispatching on the row-offset width -------------
 // dmax: largest degree in the frontier (< 0: unknown) -- the hub bin is skipped when no vertex exceeds
 // the hub degree
+// skip_hubs (hybrid level): frontier vertices of the hub domain are left to the bottom-up hub sweep.
 template <bool kDist>
-int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt) {
+int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt,
+              bool skip_hubs = false) {
     hipStream_t st = g->ctx->stream;
+    const uint32_t t_hub = ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu;
+    const uint32_t skip_deg = skip_hubs ? t_hub : 0xFFFFFFFFu;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     const uint32_t hub_deg = g->ctx->opt.hub_degree;
     int gsz = 16;
@@ -1510,34 +1582,34 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz);
+                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, t_hub, skip_deg);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt);
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, t_hub);
             BFSX_HIP_TRY(hipGetLastError());
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz);
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, t_hub, skip_deg);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt);
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, t_hub);
             BFSX_HIP_TRY(hipGetLastError());
         }
     }
     return BFSX_OK;
 }
 
-template <class OffT, bool kMf, bool kHubs, int kU>
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly>
 int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
     hipStream_t st = g->ctx->stream;
     // persistent grid: exactly the resident workgroups (a partial second wave of workgroups would
     // leave most CUs idle at the tail of the grid-stride loop)
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs, kU>, kBS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs, kU, kHubOnly>, kBS, 0) != hipSuccess ||
             per_cu < 1)
             per_cu = 4;
     }
@@ -1548,7 +1620,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
                            ws->hub_id, ws->hub_k, front, ws->hfront);
         BFSX_HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
+    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
                        ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
                        ws->top1_flag,
                        ws->hfront, ws->hub_id);
@@ -1558,8 +1630,14 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
 
 template <class OffT, bool kMf, bool kHubs>
 int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
-    return g->ctx->opt.bu_unroll == 2 ? launch_bu_u<OffT, kMf, kHubs, 2>(g, ws, row_off, front, level)
-                                      : launch_bu_u<OffT, kMf, kHubs, 4>(g, ws, row_off, front, level);
+    return g->ctx->opt.bu_unroll == 2 ? launch_bu_u<OffT, kMf, kHubs, 2, false>(g, ws, row_off, front, level)
+                                      : launch_bu_u<OffT, kMf, kHubs, 4, false>(g, ws, row_off, front, level);
+}
+
+// The bottom-up half of a hybrid level: candidates probe only the hubs of the frontier (single device).
+int launch_bu_hubonly(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
+    return ws->off32 ? launch_bu_u<uint32_t, false, true, 4, true>(g, ws, ws->off32, front, level)
+                     : launch_bu_u<int64_t, false, true, 4, true>(g, ws, g->d_row_off, front, level);
 }
 
 template <bool kMf>
@@ -1635,7 +1713,7 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         const int G = persist_blocks(g->ctx);
         ws->persist_grid = G;
         BFSX_HIP_TRY(hipMalloc(&ws->persist_seg, (size_t)2 * G * kRegion * sizeof(uint32_t)));
-        BFSX_HIP_TRY(hipMalloc(&ws->persist_brec, (size_t)2 * G * 4 * sizeof(u64)));
+        BFSX_HIP_TRY(hipMalloc(&ws->persist_brec, (size_t)2 * G * kRecWords * sizeof(u64)));
         BFSX_HIP_TRY(hipMalloc(&ws->persist_ctl, sizeof(PersistCtl)));
         BFSX_HIP_TRY(hipHostMalloc(&ws->h_pout, sizeof(PersistOut), hipHostMallocMapped | hipHostMallocCoherent));
         BFSX_HIP_TRY(hipHostGetDevicePointer(&ws->d_pout, ws->h_pout, 0));
@@ -1673,11 +1751,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
     if (ws->off32)
         hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
-                           mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout);
+                           mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
+                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
-                           mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout);
+                           mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
+                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -1746,6 +1826,9 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded (-1: unknown)
     int64_t dmax = mf;                    // its largest degree (-1: unknown)
     int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
+    // degree sum of the frontier's hub-domain vertices (-1: unknown): a top-down level whose frontier
+    // degree sum sits mostly in hubs runs as a hybrid level (below)
+    int64_t mfh = (ws->hub_k > 0 && mf >= (int64_t)ws->hub_tdeg) ? mf : 0;
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
     std::vector<LevelTiming> timing;
@@ -1769,6 +1852,66 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             ws->ev_level.push_back(e1);
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
+        // Hybrid level: a top-down level whose frontier is dominated (by degree sum) by hubs -- a hub root's
+        // neighbourhood: a few thousand vertices with tens of millions of edges -- would push every one of
+        // those edges through a random visited-bitmap probe.  Instead the unvisited vertices pull from
+        // the frontier's HUBS only (k_bu hub sweep: every probe lands in the small gathered hub bitmap,
+        // and a degree-ordered row stops at its first non-hub entry), and the frontier's non-hub
+        // vertices are expanded top-down behind it.  Measured on scale 26 (U = 32.8 M unvisited): the
+        // hybrid level costs 0.95-1.4 ms (most of it the unvisited vertices that find no frontier hub and
+        // walk their whole hub prefix), the push level ~0.028 ms per million frontier edges (0.72 ms at
+        // 17.6 M, 1.74 ms at 67.4 M) -- so hybrid only once the hubs' edges exceed 1.25 U.
+        bool hybrid = false;
+        if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && ws->hub_k > 0 && opt.hybrid != 0 && mfh > 0) {
+            const int64_t unv = nv - visited - ws->n_dead;
+            hybrid = opt.hybrid == 2 || 4 * mfh > 5 * unv;
+        }
+        if (hybrid) {
+            BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
+            hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->qa,
+                               (uint32_t)nf, ws->front);
+            BFSX_HIP_TRY(hipGetLastError());
+            if (int e = launch_bu_hubonly(g, ws, ws->front, level)) return e; // -> next, vis, st
+            const Part pt{};
+            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true)) return e; // -> qb
+            LevelSlot *cn = ws->ring + (level + 1) % 3;
+            hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, &cn->qtail, ws->next);
+            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
+            hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, cn, ws->d_pub, ++ws->pub_seq);
+            BFSX_HIP_TRY(hipGetLastError());
+            if (int e = wait_published(ws, st)) return e;
+            const int64_t nf_new = ws->h_pub->nf + ws->h_pub->qtail;
+            g->level_dirs.push_back(BFSX_DIR_HYBRID);
+            bfsx_level_stat ls{};
+            ls.direction = BFSX_DIR_HYBRID;
+            ls.level = level;
+            ls.frontier_in = nf;
+            ls.frontier_out = nf_new;
+            ls.mf_in = mf;
+            ls.unvisited_in = nv - visited - ws->n_dead;
+            ls.scanned = ws->h_pub->sc;
+            ls.claims = ws->h_pub->cl;
+            g->level_stats.push_back(ls);
+            timing.push_back({level, false, 0.0, 0.0});
+            examined += ls.scanned;
+            visited += nf_new;
+            prev_nf = nf;
+            nf = nf_new;
+            // m_u: the pull half counted the candidates it left (a row without hubs counts 1), minus the
+            // degree sum of what the push half then discovered among them
+            mu = std::max<int64_t>(ws->h_pub->mu - ws->h_pub->mf, 0);
+            mf = -1;
+            dmax = -1;
+            mfh = -1;
+            dir = BFSX_DIR_BOTTOMUP; // the new frontier is a bitmap
+            in_queue = false;
+            snapped = false;
+            bu_levels++;
+            std::swap(ws->front, ws->next);
+            if (nf == 0) break;
+            continue;
+        }
         if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
             if (snapped) { // front holds the visited bitmap from before the last top-down level
                 hipLaunchKernelGGL(k_new_bits, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
@@ -1818,6 +1961,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 nf = ls.frontier_out;
                 mf = (int64_t)r.mf;
                 dmax = (int64_t)r.dmax;
+                mfh = ws->hub_k > 0 ? (int64_t)r.mfh : -1;
             }
             std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
             td_levels += ran;
@@ -1874,11 +2018,13 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             mu -= s.mf;
             mf = s.mf;
             dmax = ws->h_pub->dmax;
+            mfh = ws->hub_k > 0 ? s.s2 : -1; // top-down: stage2 = degree sum of the hubs discovered
             std::swap(ws->qa, ws->qb);
         } else {
             mu = s.mu; // exact: degree sum of the candidates this level left unvisited
             mf = -1;   // not accumulated by the single-GPU bottom-up step
             dmax = -1;
+            mfh = -1;
             std::swap(ws->front, ws->next);
         }
         if (nf == 0) break;

@@ -48,6 +48,7 @@ extern "C" {
 #define BFSX_DIR_AUTO 0     /* direction-optimising (Beamer alpha/beta switch) */
 #define BFSX_DIR_TOPDOWN 1  /* push only: the reference mapper's direction (BfsSpark.java:73-79) */
 #define BFSX_DIR_BOTTOMUP 2 /* pull only */
+#define BFSX_DIR_HYBRID 3   /* (level records only) pull from the frontier's hubs + push from its other vertices */
 
 typedef struct bfsx_ctx bfsx_ctx;
 typedef struct bfsx_graph bfsx_graph;
@@ -99,6 +100,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU; fixed at a graph's first BFS)
  *   "hub_bits" = auto|off|1..30 (bottom-up probes of the 2^b highest-degree vertices go to a small
  *                 gathered bitmap; auto = n/1024 rounded up to a power of two; fixed at a graph's first BFS)
+ *   "hybrid" = auto|off|force (a top-down level whose frontier's edges sit mostly in hub-domain vertices
+ *                 runs as pull-from-hubs + push-from-the-rest; force = every eligible level, for tests)
+ *   "bu_unroll" = 4|2 (bottom-up candidates per lane per round)
  *   "build_chunk" = int (CSR build: raw adjacency entries per sort/dedup chunk, default 2^30; bounds the
  *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);

@@ -384,3 +384,39 @@ def test_bottomup_unroll_variants(ctx, unroll):
     finally:
         for k, val in (("bu_unroll", "4"), ("hub_bits", "auto"), ("direction", "auto")):
             ctx.set_option(k, val)
+
+
+@pytest.mark.parametrize("bits", ["2", "6", "30"])
+def test_hybrid_levels(ctx, bits):
+    """Hybrid levels (pull from the frontier's hubs + push from its other vertices; option hybrid=force
+    runs every top-down level whose frontier holds a hub that way): bit-exact distances, valid parents
+    and the same pass count, whatever the hub count (30 = every vertex is a hub: the push half is empty;
+    2 = four hubs: most of the frontier is pushed)."""
+    ctx.set_option("hub_bits", bits)
+    ctx.set_option("hybrid", "force")
+    ctx.set_option("persist", "off")  # every level through the per-level loop (persist=on is covered below)
+    try:
+        hy = 0
+        for name, nv, u, v in [c for c in random_cases() if c[0] in ("rand1", "rand4", "star", "multi_hub",
+                                                                      "two_comp", "self_loops")]:
+            u = np.asarray(u, np.uint32)
+            v = np.asarray(v, np.uint32)
+            off, col = O.build_sets(nv, u, v)
+            with ctx.from_edges(nv, u, v) as g:
+                for s in sorted({0, nv // 2, nv - 1}):
+                    check_against_oracle(g, nv, off, col, s, u, v, mr=False)
+                    assert g.validate()["errors"] == 0
+                    hy += sum(1 for d in g.level_dirs() if d == 3)
+        ou, ov = O.kronecker(14, 16, 0x5EED2026)
+        off, col = O.build_sets(1 << 14, ou, ov)
+        for persist in ("off", "on"):
+            ctx.set_option("persist", persist)
+            with ctx.kronecker(14, 16, 0x5EED2026) as g:
+                for r in g.sample_roots(4, seed=21):
+                    check_against_oracle(g, 1 << 14, off, col, int(r), ou, ov, mr=False)
+                    hy += sum(1 for d in g.level_dirs() if d == 3)
+        assert hy > 0, "no hybrid level ran"
+    finally:
+        ctx.set_option("hub_bits", "auto")
+        ctx.set_option("hybrid", "auto")
+        ctx.set_option("persist", "on")
