@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
-                                                    PersistOut *out, uint32_t t_hub) {
+                                                    PersistOut *out, uint32_t t_hub, int64_t bu_floor) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_scan[kBS + 1];
@@ -831,7 +831,8 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
         mu -= (int64_t)mf_new;
         const bool stop = nf_new == 0 || nf_new > kPersistNf ||
                           (u64)((nf_new + G - 1) / G) * dm_new > (u64)kRegion ||
-                          (alpha > 0 && (int64_t)mf_new > mu / alpha) || it + 1 >= max_levels;
+                          (alpha > 0 && (int64_t)mf_new > mu / alpha && (int64_t)mf_new > bu_floor) ||
+                          it + 1 >= max_levels;
         __syncthreads();
         if (stop) { // hand the frontier back contiguous
             const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
@@ -1690,6 +1691,12 @@ struct LevelTiming {
     double k_ms;   // K3p: the level's own span
 };
 
+// Beamer's top-down -> bottom-up test compares m_f with m_u / alpha, but a pull level also has a fixed
+// cost -- one pass over the n/64-word visited bitmap -- that the tail of a BFS (a few thousand frontier
+// edges against a few thousand unvisited ones) never recovers: 30-40 us pull levels where a push
+// level takes a few.  So a push level hands over only when its frontier has more than n/512 edges.
+int64_t bu_floor(const BfsWorkspace *ws) { return ws->nwords / 8; }
+
 // K3p geometry: at most one workgroup per CU and at most kBS (every workgroup reads all records).
 int persist_blocks(const bfsx_ctx *ctx) {
     const int want = ctx->opt.persist_blocks > 0 ? ctx->opt.persist_blocks : ctx->num_cus;
@@ -1752,12 +1759,12 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu);
+                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws));
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu);
+                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws));
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -1839,7 +1846,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     for (;; level++) {
         if (opt.direction == BFSX_DIR_AUTO && level > 0) {
             if (dir == BFSX_DIR_TOPDOWN) {
-                if (mf > mu / std::max(opt.alpha, 1)) dir = BFSX_DIR_BOTTOMUP;
+                if (mf > mu / std::max(opt.alpha, 1) && mf > bu_floor(ws)) dir = BFSX_DIR_BOTTOMUP;
             } else if (nf < nv / std::max(opt.beta, 1) && nf < prev_nf) {
                 dir = BFSX_DIR_TOPDOWN;
             }
