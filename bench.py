@@ -117,7 +117,8 @@ def measured_traffic(kernel="k_bu"):
             continue
         names = [n for n in rec.get("kernels", {}) if n == kernel or n.startswith(kernel + "<")]
         if rec.get("kernels_bfs_sha") == sha and names:
-            k = rec["kernels"][names[0]]
+            # the instantiation with the most launches (the hybrid levels' hub sweep is a second one)
+            k = max((rec["kernels"][n] for n in names), key=lambda x: x.get("launches", 0))
             out = {"traffic": round(k["traffic_B"] / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
                    "traffic_source": os.path.relpath(path, ROOT), "fetch_correction": rec.get("fetch_correction")}
             if k.get("avg_ms_trace"):  # fabric-side rate of the same launches (rocprof trace durations)
