@@ -116,6 +116,8 @@ struct BfsWorkspace {
     u64 *remote = nullptr;              // unbucketed remote pairs
     int64_t remote_cap = 0;
     u64 *d_dist_ctr = nullptr;          // kCtrWords: [0] remote tail, then count, cursor, recv count, sums
+    u64 *h_post = nullptr, *d_post = nullptr; // mapped pinned: [0] sequence, [1..] words posted by k_post
+    u64 post_seq = 0;
     u64 *sendbuf = nullptr, *recvbuf = nullptr, *fglob = nullptr; // native exchange buffers
     int64_t send_cap = 0, recv_cap = 0, fglob_words = 0;
     int64_t nnz_global = -1;
@@ -1399,6 +1401,15 @@ __global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, cons
     }
 }
 
+// Multi-GPU host reads without a D2H copy + stream synchronise: one wave copies two device ranges into
+// mapped pinned host memory and then publishes a sequence number the host spins on (as k_publish).
+__global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict__ b, int nb, u64 *post, u64 seq) {
+    for (int i = threadIdx.x; i < na + nb; i += blockDim.x) post[1 + i] = i < na ? a[i] : b[i - na];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) *(volatile u64 *)post = seq;
+}
+
 // Multi-GPU level close: one workgroup sums the level's counter shards into
 //   out[0..6] = local {n_f, m_f, m_u, scanned, rows/claims, stage2, walked}   out[8..10] = copy of {n_f, m_f, m_u}
 // (the copy is all-reduced in place; the local half stays for the per-level record).
@@ -1670,6 +1681,24 @@ int wait_published(BfsWorkspace *ws, hipStream_t st) {
     return BFSX_OK;
 }
 
+// Post `na` words at a and `nb` at b to the host (in order) and wait for them; out gets na + nb words.
+int post_wait(BfsWorkspace *ws, hipStream_t st, const u64 *a, int na, const u64 *b, int nb, u64 *out) {
+    hipLaunchKernelGGL(k_post, dim3(1), dim3(64), 0, st, a, na, b, nb, ws->d_post, ++ws->post_seq);
+    BFSX_HIP_TRY(hipGetLastError());
+    const volatile u64 *seq = ws->h_post;
+    for (uint64_t spin = 1; *seq != ws->post_seq; spin++) {
+        if ((spin & 0xFFFF) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(BFSX_E_HIP, std::string("exchange: ") + hipGetErrorString(e));
+            if (e == hipSuccess && *seq != ws->post_seq) return fail(BFSX_E_HIP, "exchange counts were not posted");
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    for (int i = 0; i < na + nb; i++) out[i] = ((const volatile u64 *)ws->h_post)[1 + i];
+    return BFSX_OK;
+}
+
 SlotSums sum_slot(const LevelSlot *s) {
     SlotSums r;
     for (int i = 0; i < kShards; i++) {
@@ -1796,6 +1825,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->h_pub) (void)hipHostFree(ws->h_pub);
     if (ws->h_pout) (void)hipHostFree(ws->h_pout);
+    if (ws->h_post) (void)hipHostFree(ws->h_post);
     if (ws->ev_start) (void)hipEventDestroy(ws->ev_start);
     if (ws->ev_end) (void)hipEventDestroy(ws->ev_end);
     for (auto e : ws->ev_level) (void)hipEventDestroy(e);
@@ -2134,6 +2164,13 @@ int dist_ws(bfsx_graph *g) {
     int rc = ws_alloc(g);
     if (rc) return rc;
     if (!g->ws->d_dist_ctr) BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, kCtrWords * sizeof(u64)));
+    if (!g->ws->h_post) {
+        BFSX_HIP_TRY(hipHostMalloc(&g->ws->h_post, (1 + 2 * kMaxRanks + 16) * sizeof(u64),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+        BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&g->ws->d_post, g->ws->h_post, 0));
+        g->ws->h_post[0] = 0;
+        g->ws->post_seq = 0;
+    }
     return BFSX_OK;
 }
 
@@ -2372,9 +2409,7 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) 
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3, st)) return e;
-    BFSX_HIP_TRY(hipMemcpyAsync(out, sums, 16 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    BFSX_HIP_TRY(hipStreamSynchronize(st));
-    return BFSX_OK;
+    return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 16, nullptr, 0, reinterpret_cast<u64 *>(out));
 }
 
 } // namespace
@@ -2477,13 +2512,11 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             u64 *drecv = ws->d_dist_ctr + kCtrRecv;
             if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
                 return e;
-            BFSX_HIP_TRY(hipMemcpyAsync(hc.data(), dcount, P * sizeof(u64), hipMemcpyDeviceToHost, st));
-            BFSX_HIP_TRY(hipMemcpyAsync(hc.data() + kMaxRanks, drecv, P * sizeof(u64), hipMemcpyDeviceToHost, st));
-            BFSX_HIP_TRY(hipStreamSynchronize(st));
+            if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
             int64_t so = 0, ro = 0;
             for (int p = 0; p < P; p++) {
                 scount[p] = (int64_t)hc[p];
-                rcount[p] = (int64_t)hc[kMaxRanks + p];
+                rcount[p] = (int64_t)hc[P + p];
                 sdispl[p] = so;
                 rdispl[p] = ro;
                 so += scount[p];
