@@ -269,6 +269,13 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         }
         return as_int(ctx->opt.persist_blocks);
     }
+    if (k == "slot_pairs") {
+        char *end = nullptr;
+        const long long x = strtoll(value, &end, 10);
+        if (!end || *end || x < 0) return fail(BFSX_E_ARG, "slot_pairs must be a pair count >= 0");
+        ctx->opt.slot_pairs = x;
+        return BFSX_OK;
+    }
     if (k == "hybrid") {
         if (v == "off") ctx->opt.hybrid = 0;
         else if (v == "auto") ctx->opt.hybrid = 1;

@@ -850,19 +850,28 @@ template <class OffT>
 __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pairs, uint32_t npairs,
                                                       const OffT *__restrict__ row_off, u64 *vis,
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
-                                                      LevelSlot *ring, int level, uint32_t lo) {
+                                                      LevelSlot *ring, int level, uint32_t lo, uint32_t slot) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ BlockQueue q;
     bq_init(q);
     __syncthreads();
     const int32_t nd = level + 1;
     u64 acc_mf = 0, attempts = 0, acc_dmax = 0;
+    // slot > 0: npairs = P * slot entries in P fixed slots of [count, slot pairs] (small levels)
     for (uint32_t i0 = blockIdx.x * kBS; i0 < npairs; i0 += gridDim.x * kBS) {
         const uint32_t i = i0 + threadIdx.x;
         bool win = false;
         uint32_t vl = 0;
-        if (i < npairs) {
-            const u64 pr = pairs[i];
+        bool have = i < npairs;
+        size_t at = i;
+        if (have && slot) {
+            const uint32_t p = i / slot, k = i - p * slot;
+            const size_t base = (size_t)p * (slot + 1);
+            have = k < pairs[base];
+            at = base + 1 + k;
+        }
+        if (have) {
+            const u64 pr = pairs[at];
             vl = (uint32_t)(pr >> 32) - lo;
             if (claim(vl, vis, attempts)) {
                 win = true;
@@ -890,6 +899,7 @@ constexpr int kCtrRecv = kCtrHead;
 constexpr int kCtrSums = kCtrHead + kMaxRanks;
 constexpr int kCtrWords = kCtrSums + 16;
 
+
 __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
                                                       uint32_t chunk, int nranks, u64 *__restrict__ dcount) {
     __shared__ uint32_t s_h[kMaxRanks];
@@ -901,6 +911,23 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pa
     __syncthreads();
     for (int d = threadIdx.x; d < nranks; d += kBS)
         if (s_h[d]) atomicAdd(&dcount[d], (u64)s_h[d]);
+}
+
+// Small top-down levels: pairs go to fixed per-destination slots of [count, cap pairs], so the exchange
+// needs no count all-to-all (and no host round trip) before the pairs move.
+__global__ __launch_bounds__(kBS) void k_bucket_slots(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
+                                                      uint32_t chunk, uint32_t cap, u64 *__restrict__ dcursor,
+                                                      u64 *__restrict__ out) {
+    const uint64_t n = *d_n;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS) {
+        const u64 pr = pairs[i];
+        const uint32_t d = (uint32_t)(pr >> 32) / chunk;
+        const u64 r = atomicAdd(&dcursor[d], 1ull);
+        out[(size_t)d * (cap + 1) + 1 + r] = pr;
+    }
+}
+__global__ void k_slot_headers(const u64 *__restrict__ dcursor, int nranks, uint32_t cap, u64 *__restrict__ out) {
+    for (int p = threadIdx.x; p < nranks; p += blockDim.x) out[(size_t)p * (cap + 1)] = dcursor[p];
 }
 
 __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
@@ -2288,10 +2315,10 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     const dim3 grid(clamp_grid((n + kBS - 1) / kBS, cap));
     if (ws->off32)
         hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (uint32_t)n, ws->off32, ws->vis,
-                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo);
+                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, 0u);
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (uint32_t)n, g->d_row_off,
-                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo);
+                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, 0u);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -2503,26 +2530,45 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
             const unsigned gbk = clamp_grid((need + kBS - 1) / kBS, 1024);
-            hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                               (uint32_t)g->chunk, P, dcount);
-            BFSX_HIP_TRY(hipGetLastError());
-            hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                               (uint32_t)g->chunk, P, dcount, dcursor, ws->sendbuf);
-            BFSX_HIP_TRY(hipGetLastError());
-            u64 *drecv = ws->d_dist_ctr + kCtrRecv;
-            if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
-                return e;
-            if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
-            int64_t so = 0, ro = 0;
-            for (int p = 0; p < P; p++) {
-                scount[p] = (int64_t)hc[p];
-                rcount[p] = (int64_t)hc[P + p];
-                sdispl[p] = so;
-                rdispl[p] = ro;
-                so += scount[p];
-                ro += rcount[p];
+            int64_t slot = 0, ro = 0; // slot > 0: fixed-slot exchange
+            if (P > 1 && mf <= opt.slot_pairs) {
+                // small level: no rank sends more than the global m_f pairs to any peer, so every peer gets
+                // a fixed slot [count, m_f pairs] -- one exchange, no count all-to-all, no host wait
+                slot = std::max<int64_t>(mf, 1);
+                if (int e = grow(ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
+                if (int e = grow(ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
+                hipLaunchKernelGGL(k_bucket_slots, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
+                                   (uint32_t)g->chunk, (uint32_t)slot, dcursor, ws->sendbuf);
+                BFSX_HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, st, dcursor, P, (uint32_t)slot, ws->sendbuf);
+                BFSX_HIP_TRY(hipGetLastError());
+                for (int p = 0; p < P; p++) {
+                    scount[p] = rcount[p] = slot + 1;
+                    sdispl[p] = rdispl[p] = p * (slot + 1);
+                }
+                ro = P * slot;
+            } else {
+                hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
+                                   (uint32_t)g->chunk, P, dcount);
+                BFSX_HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
+                                   (uint32_t)g->chunk, P, dcount, dcursor, ws->sendbuf);
+                BFSX_HIP_TRY(hipGetLastError());
+                u64 *drecv = ws->d_dist_ctr + kCtrRecv;
+                if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
+                    return e;
+                if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
+                int64_t so = 0;
+                for (int p = 0; p < P; p++) {
+                    scount[p] = (int64_t)hc[p];
+                    rcount[p] = (int64_t)hc[P + p];
+                    sdispl[p] = so;
+                    rdispl[p] = ro;
+                    so += scount[p];
+                    ro += rcount[p];
+                }
+                if (int e = grow(ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
             }
-            if (int e = grow(ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
             if (int e = cm->alltoallv(ws->sendbuf, scount.data(), sdispl.data(), ws->recvbuf, rcount.data(),
                                       rdispl.data(), st))
                 return e;
@@ -2530,10 +2576,12 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 const dim3 grid(clamp_grid((ro + kBS - 1) / kBS, cap));
                 if (ws->off32)
                     hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (uint32_t)ro,
-                                       ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo);
+                                       ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
+                                       (uint32_t)slot);
                 else
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (uint32_t)ro,
-                                       g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo);
+                                       g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
+                                       (uint32_t)slot);
                 BFSX_HIP_TRY(hipGetLastError());
             }
             td_levels++;

@@ -103,6 +103,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "hybrid" = auto|off|force (a top-down level whose frontier's edges sit mostly in hub-domain vertices
  *                 runs as pull-from-hubs + push-from-the-rest; force = every eligible level, for tests)
  *   "bu_unroll" = 4|2 (bottom-up candidates per lane per round)
+ *   "slot_pairs" = int (partitioned graphs: a push level whose frontier has at most this many edges in
+ *                 total exchanges its pairs through fixed per-peer slots, skipping the count all-to-all
+ *                 and its host wait; default 16384, 0 = never)
  *   "build_chunk" = int (CSR build: raw adjacency entries per sort/dedup chunk, default 2^30; bounds the
  *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);

@@ -152,3 +152,16 @@ print("rccl-ok")
 """
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and "rccl-ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("slot_pairs", ["0", "16384", "100000000"])
+def test_native_group_exchange_modes(bfsx, slot_pairs):
+    """Push-level pair exchange in both forms: counts all-to-all then variable sends (slot_pairs=0),
+    fixed per-peer slots for every level (huge threshold), and the default mix; all bit-exact."""
+    scale, world = 14, 3
+    u, v = O.kronecker(scale, 16, 0xABC)
+    nv = 1 << scale
+    sources = [int(u[0]), int(v[100]), int(u[5000])]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, "topdown",
+                    {"slot_pairs": slot_pairs})
+    check(nv, u, v, sources, out)
