@@ -9,6 +9,7 @@
 //       source=0 (GraphFileUtil.java:28)  device=0  direction=auto|topdown|bottomup
 //       writeInitial=true (problemFile_0, GraphFileUtil.java:68)  writePaths=true
 //       dumpLevels=false (every intermediate problemFile_<k>, BfsSpark.java:115-116)
+//       validate=false (Graph500-style check of the result on the device, bfsx_validate; logged)
 //   - input: algs4 edge lists, parsed with GraphFileUtil.convert semantics (inside libbfsx.so)
 //   - output: problemFile_<k> in Vertex.toString format  id|[n, ...]|[path]|distance|COLOR
 //     (Vertex.java:123-125), one line per vertex, k = number of map/reduce passes; the final file has
@@ -183,7 +184,7 @@ bool write_state(const std::string &file, int64_t nv, const std::vector<int64_t>
 }
 
 int run_problem(bfsx_ctx *ctx, const std::string &problem, int64_t source, bool write_initial, bool paths,
-                bool dump_levels) {
+                bool dump_levels, bool validate) {
     log_line("INFO", "main", 54, "Problem file: " + problem);
     bfsx_graph *g = nullptr;
     int rc = bfsx_graph_load_algs4(ctx, problem.c_str(), &g); // GraphFileUtil.convert (BfsSpark.java:55)
@@ -236,6 +237,17 @@ int run_problem(bfsx_ctx *ctx, const std::string &problem, int64_t source, bool 
                       st.levels, st.topdown_levels, st.bottomup_levels, st.reached, st.m_comp, st.t_bfs_ms,
                       st.t_bfs_ms > 0 ? st.m_comp / (st.t_bfs_ms * 1e6) : 0.0);
         log_line("INFO", "main", 117, msg);
+        if (validate) {
+            int64_t bad = 0, first = -1;
+            if ((rc = bfsx_validate(g, source, &bad, &first, nullptr, nullptr))) {
+                log_line("ERROR", "main", 117, std::string("validation failed to run: ") + bfsx_last_error());
+                goto out;
+            }
+            log_line(bad ? "ERROR" : "INFO", "main", 117,
+                     bad ? "Validation: " + std::to_string(bad) + " violating vertices, first " + std::to_string(first)
+                         : std::string("Validation: OK (Graph500 rules, exact BFS distances)"));
+            if (bad) rc = BFSX_E_ARG;
+        }
     }
 out:
     bfsx_graph_free(g);
@@ -287,9 +299,10 @@ int main(int argc, char **argv) {
     const bool write_initial = truthy(get("writeInitial", "true"));
     const bool paths = truthy(get("writePaths", "true"));
     const bool dump = truthy(get("dumpLevels", "false"));
+    const bool validate = truthy(get("validate", "false"));
     int status = 0;
     for (const auto &f : files) { // BfsSpark.java:53
-        rc = run_problem(ctx, f, source, write_initial, paths, dump);
+        rc = run_problem(ctx, f, source, write_initial, paths, dump, validate);
         if (rc) {
             status = rc == BFSX_E_IO ? 4 : 5;
             break; // an exception escapes main in the reference (BfsSpark.java:43 throws Exception)

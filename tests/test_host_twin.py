@@ -78,9 +78,10 @@ def test_bfs_spark_twin_end_to_end(tmp_path):
     for n in names:
         shutil.copy(os.path.join(GOLDEN, n + ".txt"), tmp_path / (n + ".txt"))
         files.append(f"{n}.txt")
-    write_props(tmp_path, files, "dumpLevels=true\n")
+    write_props(tmp_path, files, "dumpLevels=true\nvalidate=true\n")
     r = subprocess.run([BIN], cwd=tmp_path, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Validation: OK") == len(names)
     passes = {"tinyCG": 3, "mediumG": 14, "tinyG": 3}
     for n in names:
         assert f"Problem file: {n}.txt" in r.stdout
