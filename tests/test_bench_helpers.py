@@ -1,0 +1,55 @@
+"""CPU checks of bench.py's accounting (no GPU): the algorithmic-bytes model of a level,
+the harmonic mean, and the PMC traffic lookup keyed by the kernel source hash."""
+import importlib.util
+import json
+import os
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bottom_up_level_bytes(bench):
+    ls = {"direction": 2, "unvisited_in": 1000, "stage2": 100, "claims": 10, "walked": 50, "frontier_out": 600}
+    nwords = 64
+    assert bench.level_bytes(ls, nwords) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 8 * 600
+
+
+def test_top_down_level_bytes(bench):
+    ls = {"direction": 1, "frontier_in": 10, "mf_in": 300, "frontier_out": 20}
+    assert bench.level_bytes(ls, 1) == 20 * 10 + 4 * 300 + 28 * 20
+
+
+def test_hmean(bench):
+    assert bench.hmean([1.0, 1.0]) == 1.0
+    assert abs(bench.hmean([1.0, 3.0]) - 1.5) < 1e-12
+
+
+def test_measured_traffic_requires_matching_source(bench, tmp_path, monkeypatch):
+    """A PMC summary counts only while kernels_bfs.hip still hashes to the source it was measured on;
+    of several k_bu instantiations the one with the most launches is reported."""
+    import hashlib
+    src = os.path.join(ROOT, "bfs-with-mapreduce_amd", "csrc", "kernels_bfs.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    rec = {"kernels_bfs_sha": sha, "fetch_correction": 2.0,
+           "kernels": {"k_bu<a, true>": {"launches": 2, "traffic_B": 9e9, "traffic_raw_B": 5e9, "avg_ms_trace": 1.0},
+                       "k_bu<a, false>": {"launches": 90, "traffic_B": 1.2e9, "traffic_raw_B": 7e8,
+                                          "avg_ms_trace": 0.25}}}
+    (prof / "zz_hbm.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "PKG", os.path.join(ROOT, "bfs-with-mapreduce_amd"))
+    out = bench.measured_traffic()
+    assert out["traffic"] == 1200.0 and out["traffic_GBs"] == 4800.0
+    rec["kernels_bfs_sha"] = "0" * 16
+    (prof / "zz_hbm.json").write_text(json.dumps(rec))
+    assert bench.measured_traffic()["traffic"] is None
