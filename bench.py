@@ -252,7 +252,11 @@ def run_dist(args, world, rank, local_rank):
     os.dup2(2, 1)
     dist.init_process_group("gloo")
     bfsx = load_module("bfsx", "bfsx.py")
-    ctx = bfsx.Context(local_rank, direction=args.direction)
+    # one GPU per rank: local_rank indexes the visible devices (a launcher that pins each rank to its
+    # own device with HIP_VISIBLE_DEVICES leaves exactly one visible)
+    ndev = torch.cuda.device_count()
+    device = local_rank if local_rank < ndev else (local_rank % max(ndev, 1))
+    ctx = bfsx.Context(device, direction=args.direction)
     for kv in args.option:
         k, val = kv.split("=", 1)
         ctx.set_option(k, val)
