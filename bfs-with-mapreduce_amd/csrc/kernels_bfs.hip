@@ -1353,11 +1353,17 @@ __global__ __launch_bounds__(kBS) void k_rest(const int64_t *__restrict__ row_of
     }
 }
 
+// Degrees of this rank's rows as uint32, padded with 0 to `chunk` entries (the all-gather slice).
+__global__ __launch_bounds__(kBS) void k_slice_degrees(const int64_t *__restrict__ row_off, int64_t nv, int64_t chunk,
+                                                       uint32_t *__restrict__ out) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < chunk; v += (int64_t)gridDim.x * kBS)
+        out[v] = v < nv ? (uint32_t)(row_off[v + 1] - row_off[v]) : 0u;
+}
 // Hub selection: sort keys ~degree (ascending = degree descending, ties by id: the sort is stable).
-__global__ __launch_bounds__(kBS) void k_hub_keys(const int64_t *__restrict__ row_off, int64_t nv,
+__global__ __launch_bounds__(kBS) void k_hub_keys(const uint32_t *__restrict__ deg, int64_t n,
                                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
-    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
-        keys[v] = ~(uint32_t)(row_off[v + 1] - row_off[v]);
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < n; v += (int64_t)gridDim.x * kBS) {
+        keys[v] = ~deg[v];
         ids[v] = (uint32_t)v;
     }
 }
@@ -1466,56 +1472,76 @@ unsigned clamp_grid(int64_t blocks, unsigned cap) {
     return (unsigned)std::min<int64_t>(blocks, cap);
 }
 
-// Hub probe domain of k_bu (single device): the hub_k highest-degree vertices (option "hub_bits":
+// Hub probe domain of k_bu: the hub_k highest-degree vertices of the whole graph (option "hub_bits":
 // auto = the power of two >= n/1024 (measured: 2^16..2^19 hubs at scale 26 within noise, more hubs slower
-// as the per-level gather grows), off for graphs partitioned over several ranks, ids >= 2^30 or
-// n < 2^16).  The hub ranking needs every vertex's degree, which a rank of a partition does not hold.
+// as the per-level gather grows); off for ids >= 2^30 or n < 2^16).  On a partition every rank ranks the
+// global degrees and gathers the hubs' bits from the all-gathered global frontier bitmap.
 int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     const int hb = g->ctx->opt.hub_bits;
-    if (g->nranks > 1 || hb == 0 || g->nv_global > ((int64_t)1 << 30) || g->nv < 64) return BFSX_OK;
+    const bool part = g->nranks > 1;
+    if (hb == 0 || g->nv_global > ((int64_t)1 << 30) || g->nv_global < 64) return BFSX_OK;
+    Comm *cm = g->ctx->comm.get();
+    // a partition ranks the hubs by GLOBAL degree: the degrees are all-gathered over the communicator
+    // (collective -- every rank reaches this at its first BFS); a partition driven without one (the
+    // Python level-primitive driver) stays off
+    if (part && (!cm || cm->nranks != g->nranks || cm->rank != g->rank)) return BFSX_OK;
     int64_t k;
     if (hb < 0) {
-        if (g->nv < ((int64_t)1 << 16)) return BFSX_OK;
+        if (g->nv_global < ((int64_t)1 << 16)) return BFSX_OK;
         k = 64;
-        while (k * 1024 < g->nv) k *= 2;
+        while (k * 1024 < g->nv_global) k *= 2;
     } else {
         k = (int64_t)1 << hb;
     }
-    k = std::min<int64_t>(k, g->nv);
+    const int64_t ng = part ? g->chunk * g->nranks : g->nv; // ids ranked (a partition: padded slices)
+    k = std::min<int64_t>(k, ng);
     hipStream_t st = g->ctx->stream;
-    const size_t nv = (size_t)g->nv;
-    // the encoded adjacency copy (4 B per entry) and the ranking temporaries must leave half of the free
-    // device memory untouched (scale 30 on one device: the graph alone is ~150 GB), else stay off
-    size_t mfree = 0, mtotal = 0;
-    BFSX_HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
-    if ((size_t)g->nnz * 4 + nv * 20 > mfree / 2) return BFSX_OK;
+    const size_t nv = (size_t)g->nv, nr = (size_t)ng;
     struct Tmp {
         void *p = nullptr;
         ~Tmp() {
             if (p) (void)hipFree(p);
         }
-    } keys, keys2, ids, ids2, hidx, sort_tmp;
-    BFSX_HIP_TRY(hipMalloc(&keys.p, nv * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&keys2.p, nv * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ids.p, nv * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ids2.p, nv * sizeof(uint32_t)));
-    const unsigned gfill = clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192);
-    hipLaunchKernelGGL(k_hub_keys, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, (uint32_t *)keys.p,
+    } degs, slice, keys, keys2, ids, ids2, hidx, sort_tmp;
+    BFSX_HIP_TRY(hipMalloc(&degs.p, nr * sizeof(uint32_t)));
+    const unsigned gfill = clamp_grid(((int64_t)nr + kBS - 1) / kBS, 8192);
+    if (part) {
+        BFSX_HIP_TRY(hipMalloc(&slice.p, (size_t)g->chunk * sizeof(uint32_t)));
+        hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, g->chunk,
+                           (uint32_t *)slice.p);
+        BFSX_HIP_TRY(hipGetLastError());
+        if (int e = cm->allgather((const u64 *)slice.p, g->chunk / 2, (u64 *)degs.p, st)) return e;
+    } else {
+        hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, g->nv,
+                           (uint32_t *)degs.p);
+        BFSX_HIP_TRY(hipGetLastError());
+    }
+    // the encoded adjacency copy (4 B per entry) and the ranking temporaries must leave half of the free
+    // device memory untouched (scale 30 on one device: the graph alone is ~150 GB), else stay off (a
+    // local decision: a rank's hub domain only changes how ITS pull kernel probes)
+    size_t mfree = 0, mtotal = 0;
+    BFSX_HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
+    if ((size_t)g->nnz * 4 + nr * 20 > mfree / 2) return BFSX_OK;
+    BFSX_HIP_TRY(hipMalloc(&keys.p, nr * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&keys2.p, nr * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&ids.p, nr * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&ids2.p, nr * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_hub_keys, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)degs.p, ng, (uint32_t *)keys.p,
                        (uint32_t *)ids.p);
     BFSX_HIP_TRY(hipGetLastError());
     size_t tb = 0;
     BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
-                                           (uint32_t *)ids2.p, nv, 0, 32, st));
+                                           (uint32_t *)ids2.p, nr, 0, 32, st));
     BFSX_HIP_TRY(hipMalloc(&sort_tmp.p, std::max<size_t>(tb, 16)));
     BFSX_HIP_TRY(rocprim::radix_sort_pairs(sort_tmp.p, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
-                                           (uint32_t *)ids2.p, nv, 0, 32, st));
+                                           (uint32_t *)ids2.p, nr, 0, 32, st));
     // the hub set is closed under degree ties: every vertex of degree >= the k-th largest degree (so a
     // kernel tells a hub by its degree alone, and degree-ordered rows hold their hubs as a prefix)
     uint32_t kth = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&kth, (uint32_t *)keys2.p + (k - 1), sizeof(kth), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
-    hipLaunchKernelGGL(k_count_le, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)keys2.p, g->nv, kth, ws->d_red);
+    hipLaunchKernelGGL(k_count_le, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)keys2.p, ng, kth, ws->d_red);
     BFSX_HIP_TRY(hipGetLastError());
     u64 keff = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&keff, ws->d_red, sizeof(keff), hipMemcpyDeviceToHost, st));
@@ -1524,8 +1550,8 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     ws->hub_tdeg = ~kth;
     BFSX_HIP_TRY(hipMalloc(&ws->hub_id, (size_t)k * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMemcpyAsync(ws->hub_id, ids2.p, (size_t)k * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    BFSX_HIP_TRY(hipMalloc(&hidx.p, nv * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMemsetAsync(hidx.p, 0xFF, nv * sizeof(uint32_t), st));
+    BFSX_HIP_TRY(hipMalloc(&hidx.p, nr * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMemsetAsync(hidx.p, 0xFF, nr * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_hub_index, dim3(clamp_grid((k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->hub_id, k,
                        (uint32_t *)hidx.p);
     BFSX_HIP_TRY(hipGetLastError());
@@ -1533,8 +1559,8 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid((g->nnz + kBS - 1) / kBS, 65536)), dim3(kBS), 0, st, g->d_col,
                        g->nnz, (const uint32_t *)hidx.p, 0u, ws->colh);
     BFSX_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_hub_encode, dim3(gfill), dim3(kBS), 0, st, ws->top1, g->nv, (const uint32_t *)hidx.p,
-                       ws->top1_flag, ws->top1);
+    hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                       ws->top1, g->nv, (const uint32_t *)hidx.p, ws->top1_flag, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipMalloc(&ws->hfront, (size_t)((k + 63) / 64) * sizeof(u64)));
     BFSX_HIP_TRY(hipStreamSynchronize(st)); // the temporaries are freed on return

@@ -165,3 +165,19 @@ def test_native_group_exchange_modes(bfsx, slot_pairs):
     out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, "topdown",
                     {"slot_pairs": slot_pairs})
     check(nv, u, v, sources, out)
+
+
+@pytest.mark.parametrize("world,bits", [(2, "3"), (3, "8"), (4, "30")])
+def test_native_group_hub_domain(bfsx, world, bits):
+    """The bottom-up hub probe domain on a partition: hubs ranked by GLOBAL degree (all-gathered at the
+    first BFS), their bits gathered from the all-gathered frontier; bit-exact in pull-only and auto."""
+    rng = np.random.default_rng(7 + world)
+    nv = 5000
+    hubs = rng.integers(0, nv, 40)
+    u = np.r_[rng.integers(0, nv, 4 * nv), np.repeat(hubs, 300)].astype(np.uint32)
+    v = np.r_[rng.integers(0, nv, 4 * nv), rng.integers(0, nv, 40 * 300)].astype(np.uint32)
+    sources = [0, int(hubs[0]), 4321]
+    for direction in ("bottomup", "auto"):
+        out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, direction,
+                        {"hub_bits": bits})
+        check(nv, u, v, sources, out)
