@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libbfsx.so")
+# BFSX_LIB: another build of the same library (A/B timing of two builds on one box)
+LIB_PATH = os.environ.get("BFSX_LIB") or os.path.join(PKG_DIR, "libbfsx.so")
 
 BFSX_OK = 0
 BFSX_E_IO = -1
