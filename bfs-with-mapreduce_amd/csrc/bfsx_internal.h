@@ -80,7 +80,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
 // multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
-int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local);
+int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
 int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue);
 int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, int64_t *send_counts);
 int dist_td_claim(bfsx_graph *g, const unsigned long long *d_recv, int64_t n);

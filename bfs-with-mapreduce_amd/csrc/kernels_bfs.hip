@@ -121,6 +121,7 @@ struct BfsWorkspace {
     u64 *sendbuf = nullptr, *recvbuf = nullptr, *fglob = nullptr; // native exchange buffers
     int64_t send_cap = 0, recv_cap = 0, fglob_words = 0;
     int64_t nnz_global = -1;
+    std::vector<uint32_t> h_gdeg;       // partitioned: global degree of every id (rank p's slice at p * chunk)
     int d_level = 0, d_dir = BFSX_DIR_TOPDOWN;
     bool d_in_queue = true;
     int64_t d_nf = 0, d_mf = 0;
@@ -2240,7 +2241,9 @@ int dist_level_events(BfsWorkspace *ws, int level) {
 
 } // namespace
 
-int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local) {
+// deg_known >= 0: the source's degree (the native loop reads its host degree table), so the owner
+// needs no D2H read of its row bounds
+int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known) {
     if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
     int rc = dist_ws(g);
     if (rc) return rc;
@@ -2249,7 +2252,9 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local) {
     const bool owned = source >= g->v_lo && source < g->v_lo + g->nv;
     const int64_t sl = owned ? source - g->v_lo : -1;
     int64_t deg = 0;
-    if (owned) {
+    if (owned && deg_known >= 0) {
+        deg = deg_known;
+    } else if (owned) {
         int64_t so[2];
         BFSX_HIP_TRY(hipMemcpy(so, g->d_row_off + sl, sizeof(so), hipMemcpyDeviceToHost));
         deg = so[1] - so[0];
@@ -2490,14 +2495,33 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
         ws->nnz_global = h[0];
     }
+    if (ws->h_gdeg.empty()) {
+        // once per graph (collective): every rank's slice degrees, all-gathered into a host table, so a
+        // BFS learns its source's global degree (the first level's m_f) with no collective or host wait
+        const int64_t ng = g->chunk * P;
+        u64 *slice = nullptr, *all = nullptr;
+        BFSX_HIP_TRY(hipMalloc(&slice, g->chunk * sizeof(uint32_t)));
+        BFSX_HIP_TRY(hipMalloc(&all, ng * sizeof(uint32_t)));
+        hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                           g->d_row_off, g->nv, g->chunk, reinterpret_cast<uint32_t *>(slice));
+        int e = hipGetLastError() == hipSuccess ? cm->allgather(slice, g->chunk / 2, all, st) : BFSX_E_HIP;
+        if (!e) {
+            ws->h_gdeg.resize(ng);
+            if (hipMemcpyAsync(ws->h_gdeg.data(), all, ng * sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                e = fail(BFSX_E_HIP, "degree table copy");
+        }
+        (void)hipFree(slice);
+        (void)hipFree(all);
+        if (e) {
+            ws->h_gdeg.clear();
+            return e;
+        }
+    }
+    if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
+    const int64_t deg = ws->h_gdeg[source]; // global ids index the padded slices directly (v_lo = rank * chunk)
     int64_t deg_local = 0;
-    if ((rc = dist_begin(g, source, &deg_local))) return rc;
-    h[0] = deg_local;
-    BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    if (int e = cm->allreduce_sum(sums + 8, 1, st)) return e;
-    BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    BFSX_HIP_TRY(hipStreamSynchronize(st));
-    const int64_t deg = h[0];
+    if ((rc = dist_begin(g, source, &deg_local, deg))) return rc;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     int64_t nf = 1, prev_nf = 0, mf = deg, mu = ws->nnz_global - deg, examined = 0;
