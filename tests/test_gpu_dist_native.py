@@ -181,3 +181,43 @@ def test_native_group_hub_domain(bfsx, world, bits):
         out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, direction,
                         {"hub_bits": bits})
         check(nv, u, v, sources, out)
+
+
+def test_native_group_source_degrees(bfsx):
+    """The partitioned loop reads a BFS's source degree from its host degree table (every id's degree,
+    all-gathered once per graph): sources of degree 0, in the last rank's partly padded slice, and of
+    the largest degree all give the oracle's distances; an id outside the graph fails on every rank."""
+    rng = np.random.default_rng(31)
+    nv = 5003  # not a multiple of 64 * world: the last slice is padded
+    u = rng.integers(0, nv - 40, 4 * nv).astype(np.uint32)  # the last 40 ids are isolated
+    v = rng.integers(0, nv - 40, 4 * nv).astype(np.uint32)
+    deg = np.bincount(np.concatenate([u, v]), minlength=nv)
+    sources = [nv - 1, nv - 41, int(np.argmax(deg)), 0]
+    out = run_group(bfsx, 3, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources)
+    check(nv, u, v, sources, out)
+    assert out[0][0]["levels"] == 1 and out[0][0]["reached"] == 1
+    ctxs = [bfsx.Context(0) for _ in range(2)]
+    graphs = []
+    try:
+        bfsx.local_group(ctxs)
+        graphs = [ctxs[r].dist_from_edges(nv, u, v, r, 2) for r in range(2)]
+        errs = [None, None]
+
+        def work(r):
+            try:
+                graphs[r].dist_bfs(nv)
+            except Exception as e:  # noqa: BLE001 -- expected
+                errs[r] = str(e)
+
+        ths = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=120)
+        assert all(not t.is_alive() for t in ths), "rank thread hung"
+        assert all(e is not None and "outside" in e for e in errs), errs
+    finally:
+        for g in graphs:
+            g.free()
+        for c in ctxs:
+            c.close()
