@@ -429,7 +429,12 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             u = qin[i];
             beg = (int64_t)row_off[u];
             int64_t d = (int64_t)row_off[u + 1] - beg;
-            if (d >= (int64_t)skip_deg) { // hybrid level: the bottom-up hub sweep covers this vertex
+            if (d == 1 && level > 0) {
+                // a discovered vertex with one neighbour: that neighbour is the parent it was found
+                // from (visited), so its row holds nothing to claim -- the frontier a pull level hands to
+                // a push level is mostly such leaves
+                d = 0;
+            } else if (d >= (int64_t)skip_deg) { // hybrid level: the bottom-up hub sweep covers this vertex
                 d = 0;
             } else if (d > (int64_t)hub_deg) {
                 hubs[atomicAdd(&cn->nhub, 1ull)] = u;
