@@ -420,3 +420,30 @@ def test_hybrid_levels(ctx, bits):
         ctx.set_option("hub_bits", "auto")
         ctx.set_option("hybrid", "auto")
         ctx.set_option("persist", "on")
+
+
+@pytest.mark.parametrize("direction", ["topdown", "auto", "bottomup"])
+def test_degree_one_vertices(ctx, direction):
+    """k_td gives a discovered degree-1 vertex an empty row (its one neighbour is its parent).  The
+    source itself is never skipped: BFS from a degree-1 source (a path's end, a star's leaf, a
+    caterpillar's foot) reaches everything, with the oracle's distances, valid parents and pass count."""
+    ctx.set_option("direction", direction)
+    try:
+        n = 3000
+        path_u = np.arange(n - 1, dtype=np.uint32)
+        star_u = np.zeros(n - 1, np.uint32)
+        # caterpillar: a spine 0..999, every spine vertex with two feet
+        spine = np.arange(999, dtype=np.uint32)
+        feet = np.arange(1000, 3000, dtype=np.uint32)
+        cat_u = np.concatenate([spine, (feet - 1000) // 2]).astype(np.uint32)
+        cat_v = np.concatenate([spine + 1, feet]).astype(np.uint32)
+        cases = [("path", path_u, path_u + 1, [0, n - 1]), ("star", star_u, np.arange(1, n, dtype=np.uint32), [7, 0]),
+                 ("caterpillar", cat_u, cat_v, [1000, 2999, 0])]
+        for name, u, v, sources in cases:
+            off, col = O.build_sets(n, u, v)
+            with ctx.from_edges(n, u, v) as g:
+                for s in sources:
+                    assert off[s + 1] - off[s] == 1 or name == "star" or s == 0
+                    check_against_oracle(g, n, off, col, s, u, v, mr=False)
+    finally:
+        ctx.set_option("direction", "auto")
