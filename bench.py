@@ -1,15 +1,19 @@
-"""Benchmark: GTEPS (harmonic mean over roots) on Graph500 Kronecker scale-26, edgefactor 16.
+"""Benchmark: GTEPS (harmonic mean over 64 roots) on Graph500 Kronecker scale-26, edgefactor 16.
 
-A "step" is one BFS from one root over the device-resident CSR (BASELINE.json configs[3]); the graph
-is generated and built on the GPU before the timed region.  TEPS per root = m_comp / t with m_comp =
-the input tuples inside the root's component (Graph500 convention); value = harmonic mean GTEPS over
-the K timed roots (= K*m / sum t when every root lies in the giant component).
+BASELINE.json configs[3].  The graph is generated and built on the GPU before the timed region.  A
+"step" is one Graph500 BFS pass: one BFS from EACH of the 64 sampled roots (every root validated on the
+device beforehand), so every step covers the metric's 64 roots.  TEPS per BFS = m_comp / t with m_comp =
+the input tuples inside the root's component (Graph500 convention); value = harmonic mean GTEPS over the
+K x 64 timed BFS runs.
 
-  N = 1: t = device time from source init to the last level (hipEvents inside libbfsx.so).
-  N > 1: launched as one process per GPU (torch.distributed.run); the graph is 1-D partitioned over
-         the ranks and libbfsx runs the level loop with its own RCCL communicator (all-to-allv of
-         owner-routed pairs, all-gather of frontier bitmaps, all-reduce of the level counters);
-         t = the max over ranks of the wall time of one BFS, bracketed by barrier + device sync.
+  t (both N = 1 and N > 1) = device time from source init to the last level (hipEvents inside
+  libbfsx.so); at N > 1 the per-root time is the MAX over ranks (every BFS is collective).  The
+  wall-clock aggregate over the barrier-bracketed K steps is reported next to it (value_wall).
+  N = 1: single-device level loop.  A partitioned-path rehearsal on the same device (RCCL communicator
+         of one, the loop N > 1 runs) is reported as "partitioned_p1".
+  N > 1: one process per GPU (torch.distributed.run); the graph is 1-D partitioned over the ranks and
+         libbfsx runs the level loop with its own RCCL communicator (all-to-allv of owner-routed pairs,
+         all-gather of frontier bitmaps, all-reduce of the level counters).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
 
@@ -37,18 +41,25 @@ def load_module(name, file):
     return mod
 
 
-def level_bytes(ls, nwords):
-    """Algorithmic bytes of one level."""
-    if ls["direction"] == 2:  # bottom-up: visited word read + next word write, top1 of every live
-        # candidate, rest[] (2nd..4th neighbours + degree, 16 B) of every top1 miss, the uint32 offset pair
-        # of each row walked past its first four entries (`claims`), the adjacency entries walked there,
-        # the packed state word of every vertex found.  Frontier-bit probes are not counted: the 8 MiB
-        # bitmap is cache-resident.
-        return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 16 * ls["stage2"] + 8 * ls["claims"]
+def level_bytes(ls, nwords, off_bytes=4):
+    """Algorithmic bytes of one level: what the level must move at minimum, counted from
+    its device counters.  Frontier-bit and visited-bit probes are not counted (the n/8-byte bitmaps are
+    cache-resident).  off_bytes: width of the row offsets the traversal kernels read (uint32 when the
+    graph has < 2^32 adjacency entries)."""
+    d = ls["direction"]
+    if d == 2:  # bottom-up: visited word read + next word write, top1 of every live candidate, rest[]
+        # (2nd..4th neighbours + degree, 16 B) of every top1 miss, the offset pair of each row walked past
+        # its first four entries (`claims`), the adjacency entries walked there, the packed state word
+        # of every vertex found
+        return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 16 * ls["stage2"] + 2 * off_bytes * ls["claims"]
                 + 4 * ls["walked"] + 8 * ls["frontier_out"])
-    # top-down: queue read, row offsets (2 x 8 B per frontier vertex), adjacency rows, winners'
-    # dist+parent writes, queue append, degree lookups of the winners
-    return 20 * ls["frontier_in"] + 4 * max(ls["mf_in"], 0) + 28 * ls["frontier_out"]
+    if d == 3:  # hybrid: the pull half's bitmap pass + top1 of the live candidates, the push half's rows,
+        # the state word of every vertex found
+        return 16 * nwords + 4 * max(ls["unvisited_in"], 0) + 4 * max(ls["scanned"], 0) + 8 * ls["frontier_out"]
+    # top-down: queue read + offset pair per frontier vertex, adjacency rows, winners' packed state write,
+    # queue append and offset pair (degree) lookup
+    return ((4 + 2 * off_bytes) * ls["frontier_in"] + 4 * max(ls["mf_in"], 0)
+            + (12 + 2 * off_bytes) * ls["frontier_out"])
 
 
 def hmean(xs):
@@ -58,14 +69,17 @@ def hmean(xs):
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=10, help="timed steps (one step = one BFS per root)")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--roots", type=int, default=64, help="roots per step (the metric's 64)")
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED2026)
     ap.add_argument("--root-seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--serial-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-p1", action="store_true", help="skip the partitioned-path P=1 rehearsal at N=1")
     ap.add_argument("--direction", default="auto")
     ap.add_argument("--levels-json", default="")
     ap.add_argument("--option", action="append", default=[], help="libbfsx option key=value")
@@ -75,7 +89,7 @@ def parse_args():
 
 def common_fields(args, world, value, wall, nv, m, nnz, nroots, parallelism):
     return {
-        "metric": f"GTEPS (harmonic mean, {args.steps} roots) on RMAT scale-{args.scale}",
+        "metric": f"GTEPS (harmonic mean, {nroots} roots) on RMAT scale-{args.scale}",
         "value": value,
         "unit": "GTEPS",
         "n_gpus": world,
@@ -96,6 +110,7 @@ def common_fields(args, world, value, wall, nv, m, nnz, nroots, parallelism):
             "m_tuples": m,
             "nnz_directed": nnz,
             "roots": nroots,
+            "step": f"one BFS from each of the {nroots} roots",
             "direction": args.direction,
             "parallelism": parallelism,
         },
@@ -128,24 +143,164 @@ def measured_traffic(kernel="k_bu"):
     return {"traffic": None, "traffic_source": "no PMC summary for this kernel source"}
 
 
-def roofline(bu_bytes, bu_ms, bu_launches, note):
-    ach = (bu_bytes / bu_launches) / ((bu_ms / bu_launches) * 1e-3) / 1e9 if bu_launches else 0.0
-    tr = measured_traffic()
-    return {
-        "bound": "hbm",
-        "kernel": "k_bu (bottom-up pull)",
-        "achieved": round(ach, 1),
-        "peak": PEAK_HBM_GBS,
-        "unit": "GB/s",
-        "frac": round(ach / PEAK_HBM_GBS, 4),
-        "traffic": tr.pop("traffic"),
-        "traffic_unit": "MB per launch (FETCH_SIZE x correction + WRITE_SIZE)",
-        "algorithmic": round(bu_bytes / max(bu_launches, 1) / 1e6, 1),
-        **tr,
-        "launches": bu_launches,
-        "avg_launch_ms": round(bu_ms / max(bu_launches, 1), 4),
-        "note": note,
+class LevelAccount:
+    """Algorithmic bytes of the timed BFS runs: per bottom-up launch (the dominant kernel) and summed
+    over every level of every BFS (the whole-BFS figure)."""
+
+    def __init__(self, nwords, off_bytes):
+        self.nwords, self.off_bytes = nwords, off_bytes
+        self.bu_bytes, self.bu_ms, self.bu_launches = 0, 0.0, 0
+        self.all_bytes = 0
+        self.by_dir = {1: 0, 2: 0, 3: 0}
+
+    def add(self, levels):
+        for ls in levels:
+            b = level_bytes(ls, self.nwords, self.off_bytes)
+            self.all_bytes += b
+            self.by_dir[ls["direction"]] = self.by_dir.get(ls["direction"], 0) + b
+            if ls["direction"] == 2:
+                self.bu_bytes += b
+                self.bu_ms += ls["kernel_ms"]
+                self.bu_launches += 1
+
+    def roofline(self, note):
+        n = self.bu_launches
+        ach = (self.bu_bytes / n) / ((self.bu_ms / n) * 1e-3) / 1e9 if n else 0.0
+        tr = measured_traffic()
+        return {
+            "bound": "hbm",
+            "kernel": "k_bu (bottom-up pull)",
+            "achieved": round(ach, 1),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4),
+            "traffic": tr.pop("traffic"),
+            "traffic_unit": "MB per launch (FETCH_SIZE x correction + WRITE_SIZE)",
+            "algorithmic": round(self.bu_bytes / max(n, 1) / 1e6, 1),
+            **tr,
+            "launches": n,
+            "avg_launch_ms": round(self.bu_ms / max(n, 1), 4),
+            "note": note,
+        }
+
+    def whole(self, t_sum_ms, nbfs):
+        ach = self.all_bytes / (t_sum_ms * 1e-3) / 1e9 if t_sum_ms > 0 else 0.0
+        return {
+            "bound": "hbm",
+            "achieved": round(ach, 1),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4),
+            "algorithmic_MB_per_bfs": round(self.all_bytes / max(nbfs, 1) / 1e6, 2),
+            "by_direction_MB_per_bfs": {k: round(v / max(nbfs, 1) / 1e6, 2)
+                                        for k, v in (("push", self.by_dir.get(1, 0)), ("pull", self.by_dir.get(2, 0)),
+                                                     ("hybrid", self.by_dir.get(3, 0)))},
+            "note": "sum of every level's algorithmic bytes (push, pull and hybrid levels, from the device "
+                    "counters) over the sum of t_bfs, all timed BFS runs",
+        }
+
+
+def edge_scan_equivalent(m, nv, t_mean_ms):
+    b = 8.0 * m + 12.0 * nv
+    ach = b / (t_mean_ms * 1e-3) / 1e9
+    return {"model": "B = 4*(2M) + 12*n per BFS (SURVEY 8d edge-scan model)", "achieved_GBs": round(ach, 1),
+            "frac_of_peak": round(ach / PEAK_HBM_GBS, 4),
+            "note": "NOT a bound: an equivalent rate for the bytes a full edge scan would move. Direction "
+                    "optimisation skips most edges, so this can exceed 1.0 of peak; see whole_bfs_roofline for "
+                    "the bytes actually counted"}
+
+
+def cpu_baselines(args, g, roots, mcomp, nv):
+    """CPU rows on the host cores (rank 0, N = 1): the OpenMP restatement of the BfsSpark map/reduce
+    loop and the serial queue BFS of BreadthFirstPaths (SequentialTest.java:24-27), bounded samples."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O  # cpu_baseline leg only
+
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    nthreads = env_threads or affinity
+    off, col = g.csr()
+    samples, spent = [], 0.0
+    for r in roots:
+        c0 = time.perf_counter()
+        res = O.mapreduce_bfs(nv, off, col, int(r), nthreads=nthreads, max_iters=1)
+        dt = time.perf_counter() - c0
+        d_gpu = g.bfs(int(r), want_parent=False)[0]
+        assert np.array_equal(res["dist"], d_gpu), "CPU oracle and GPU disagree"
+        samples.append(mcomp[int(r)] / dt / 1e9)
+        spent += dt
+        if spent >= args.cpu_baseline_seconds:
+            break
+    cpu = {
+        "value": hmean(samples),
+        "unit": "GTEPS",
+        "cores": nthreads,
+        "nproc": nproc,
+        "affinity_cpus": affinity,
+        "threads_from": "OMP_NUM_THREADS" if env_threads else "sched_getaffinity",
+        "kind": "port",
+        "sample": f"{len(samples)} root(s) of the same scale-{args.scale} graph, oracle orc_mapreduce_bfs "
+                  f"(BfsSpark map/reduce restated, OpenMP), {spent:.1f} s; distances asserted equal to the GPU's",
     }
+    ser, spent_s = [], 0.0
+    for r in roots:
+        if spent_s >= args.serial_baseline_seconds:
+            break
+        c0 = time.perf_counter()
+        d_ser, _ = O.csr_bfs(nv, off, col, int(r))
+        dt = time.perf_counter() - c0
+        d_gpu = g.bfs(int(r), want_parent=False)[0]
+        assert np.array_equal(d_ser, d_gpu), "serial CPU BFS and GPU disagree"
+        ser.append(mcomp[int(r)] / dt / 1e9)
+        spent_s += dt
+    serial = {
+        "value": hmean(ser) if ser else None,
+        "unit": "GTEPS",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{len(ser)} root(s), oracle orc_csr_bfs: the FIFO-queue BFS of BreadthFirstPaths "
+                  f"(algs4.jar!/BreadthFirstPaths.java:93-111, SequentialTest.java:24-27) on the same CSR, one "
+                  f"host core, {spent_s:.1f} s; distances asserted equal to the GPU's",
+    }
+    del off, col
+    return cpu, serial
+
+
+def p1_rehearsal(args, bfsx, roots):
+    """The partitioned level loop (what N > 1 runs) at P = 1 on this device with an RCCL communicator of
+    one: the same roots, validated, the same device-time basis."""
+    ctx = bfsx.Context(0, direction=args.direction)
+    try:
+        for kv in args.option:
+            k, val = kv.split("=", 1)
+            ctx.set_option(k, val)
+        ctx.comm_init(0, 1, bfsx.comm_unique_id())
+        g = ctx.dist_kronecker(args.scale, 0, 1, args.edgefactor, args.seed)
+        mc, errs = {}, 0
+        for r in roots:
+            mc[r] = g.dist_bfs(r)["m_comp"]
+            errs += g.validate()["errors"]
+        assert errs == 0, f"partitioned P=1 validation failed: {errs}"
+        for r in roots:
+            g.dist_bfs(r, want_stats=False)
+        ctx.synchronize()
+        w0 = time.perf_counter()
+        ts = [g.dist_bfs(r, want_stats=False) for _ in range(max(1, min(args.steps, 4))) for r in roots]
+        ctx.synchronize()
+        wall = time.perf_counter() - w0
+        order = [r for _ in range(max(1, min(args.steps, 4))) for r in roots]
+        g.free()
+        return {"value": hmean([mc[r] / (t * 1e-3) / 1e9 for r, t in zip(order, ts)]), "unit": "GTEPS",
+                "value_wall": sum(mc[r] for r in order) / wall / 1e9, "bfs_runs": len(order),
+                "validated_roots": len(roots), "t_bfs_ms_mean": float(np.mean(ts)),
+                "note": "bfsx_dist_bfs with an RCCL communicator of one on the same device: the N > 1 level loop "
+                        "with its per-level collectives"}
+    finally:
+        ctx.close()
 
 
 def run_single(args):
@@ -158,84 +313,71 @@ def run_single(args):
     g = ctx.kronecker(args.scale, args.edgefactor, args.seed)
     build_s = time.perf_counter() - t0
     nv, nwords = g.nv, (g.nv + 63) // 64
-    roots = g.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)
+    off_bytes = 4 if g.nnz < 0xFFFFFFFF and "offset_bits=64" not in args.option else 8
+    roots = [int(r) for r in g.sample_roots(args.roots, seed=args.root_seed)]
     # untimed pass: m_comp per root (Graph500 counts input tuples inside the root's component)
     # and Graph500-style validation of every root's result on the device (bfsx_validate: a result that
     # passes holds exactly the graph's BFS distances)
     mcomp, val_errors = {}, 0
     for r in roots:
-        _, _, st = g.bfs(int(r), want_dist=False, want_parent=False)
-        mcomp[int(r)] = st["m_comp"]
+        _, _, st = g.bfs(r, want_dist=False, want_parent=False)
+        mcomp[r] = st["m_comp"]
         val_errors += g.validate()["errors"]
     assert val_errors == 0, f"validation failed: {val_errors} violating vertices"
-    order = [int(roots[i % len(roots)]) for i in range(args.warmup + args.steps)]
-    for r in order[: args.warmup]:
-        g.bfs_device_only(r)
+    for _ in range(args.warmup):
+        for r in roots:
+            g.bfs_device_only(r)
 
+    acct = LevelAccount(nwords, off_bytes)
     ctx.synchronize()
     w0 = time.perf_counter()
-    t_bfs, bu_bytes, bu_ms, bu_launches, all_levels = [], 0, 0.0, 0, []
-    for r in order[args.warmup:]:
-        t_bfs.append(g.bfs_device_only(r))
-        for ls in g.level_stats(256):
-            if ls["direction"] == 2:
-                bu_bytes += level_bytes(ls, nwords)
-                bu_ms += ls["kernel_ms"]
-                bu_launches += 1
+    t_bfs, order, all_levels = [], [], []
+    for _ in range(args.steps):
+        for r in roots:
+            t_bfs.append(g.bfs_device_only(r))
+            order.append(r)
+            lv = g.level_stats(256)
+            acct.add(lv)
             if args.levels_json:
-                all_levels.append(dict(ls, root=r))
+                all_levels.extend(dict(ls, root=r) for ls in lv)
     ctx.synchronize()
     wall = time.perf_counter() - w0
 
-    steps_roots = order[args.warmup:]
-    gteps = [mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(steps_roots, t_bfs)]
-    bfs_bytes = 8.0 * g.m + 12.0 * nv  # SURVEY 8(d) edge-scan model: B = 4*(2M) + 12*n per BFS
-    bfs_ach = bfs_bytes / (np.mean(t_bfs) * 1e-3) / 1e9
-
-    cpu = None
+    gteps = [mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(order, t_bfs)]
+    cpu = serial = None
     if not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_py as O  # cpu_baseline leg only
-
-        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        off, col = g.csr()
-        samples, spent = [], 0.0
-        for r in roots:
-            c0 = time.perf_counter()
-            res = O.mapreduce_bfs(nv, off, col, int(r), nthreads=nthreads, max_iters=1)
-            dt = time.perf_counter() - c0
-            d_gpu = g.bfs(int(r), want_parent=False)[0]
-            assert np.array_equal(res["dist"], d_gpu), "CPU oracle and GPU disagree"
-            samples.append(mcomp[int(r)] / dt / 1e9)
-            spent += dt
-            if spent >= args.cpu_baseline_seconds:
-                break
-        cpu = {
-            "value": hmean(samples),
-            "unit": "GTEPS",
-            "cores": nthreads,
-            "kind": "port",
-            "sample": f"{len(samples)} root(s) of the same scale-{args.scale} graph, oracle orc_mapreduce_bfs "
-                      f"(BfsSpark map/reduce restated, OpenMP), {spent:.1f} s; distances asserted equal to the GPU's",
-        }
-        del off, col
+        cpu, serial = cpu_baselines(args, g, roots, mcomp, nv)
 
     out = common_fields(args, 1, hmean(gteps), wall, nv, g.m, g.nnz, len(roots), "single")
-    out["roofline"] = roofline(bu_bytes, bu_ms, bu_launches,
-                               "algorithmic bytes of every bottom-up level / its hipEvent duration")
-    out["bfs_roofline"] = {"model": "B = 4*(2M) + 12*n per BFS (SURVEY 8d)",
-                           "achieved_GBs": round(bfs_ach, 1), "frac": round(bfs_ach / PEAK_HBM_GBS, 4)}
+    out["value_wall"] = sum(mcomp[r] for r in order) / wall / 1e9
+    out["roofline"] = acct.roofline("algorithmic bytes of every bottom-up level / its hipEvent duration")
+    out["whole_bfs_roofline"] = acct.whole(float(np.sum(t_bfs)), len(t_bfs))
+    out["edge_scan_equivalent"] = edge_scan_equivalent(g.m, nv, float(np.mean(t_bfs)))
     out.update({"t_bfs_ms_mean": float(np.mean(t_bfs)), "t_bfs_ms_min": float(np.min(t_bfs)),
-                "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])), "graph_build_s": round(build_s, 3),
+                "bfs_runs": len(t_bfs), "m_comp_mean": float(np.mean([mcomp[r] for r in order])),
+                "graph_build_s": round(build_s, 3),
                 "validation": {"roots": len(roots), "errors": val_errors,
                                "rules": "Graph500 kernel-2 + BreadthFirstPaths.check, on device (bfsx_validate)"},
-                "cpu_baseline": cpu})
+                "cpu_baseline": cpu, "cpu_baseline_serial": serial})
     if args.levels_json:
         with open(args.levels_json, "w") as f:
             json.dump(all_levels, f)
-    print(json.dumps(out), flush=True)
     g.free()
+    if not args.no_p1:
+        # RCCL prints its banner on the process's C-level stdout; the contract is ONE JSON line
+        sys.stdout.flush()
+        real_stdout = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            out["partitioned_p1"] = p1_rehearsal(args, bfsx, roots)
+        except (bfsx.BfsxError, AssertionError) as e:
+            out["partitioned_p1"] = {"error": str(e)}
+        finally:
+            sys.stdout.flush()
+            os.dup2(real_stdout, 1)
+            os.close(real_stdout)
     ctx.close()
+    print(json.dumps(out), flush=True)
 
 
 def run_dist(args, world, rank, local_rank):
@@ -268,51 +410,51 @@ def run_dist(args, world, rank, local_rank):
     ctx.synchronize()
     build_s = time.perf_counter() - t0
     part = g.partition()
-    roots = [int(r) for r in g.sample_roots(min(max(args.steps, 1), 64), seed=args.root_seed)]
+    roots = [int(r) for r in g.sample_roots(args.roots, seed=args.root_seed)]
     mcomp, val_errors = {}, 0
     for r in roots:  # untimed, collective: m_comp and Graph500-style validation of every root
         mcomp[r] = g.dist_bfs(r)["m_comp"]
         val_errors += g.validate()["errors"]
     assert val_errors == 0, f"validation failed: {val_errors} violating vertices"
-    order = [roots[i % len(roots)] for i in range(args.warmup + args.steps)]
-    for r in order[: args.warmup]:
-        g.dist_bfs(r, want_stats=False)
+    for _ in range(args.warmup):
+        for r in roots:
+            g.dist_bfs(r, want_stats=False)
 
-    # The K roots run back to back between two barrier + device-synchronise brackets (the contract's
-    # timed region); every BFS is collective, so the ranks stay in step through its RCCL calls and a
-    # per-root host barrier would only add its own skew to the measurement.
+    off_bytes = 4 if g.nnz < 0xFFFFFFFF and "offset_bits=64" not in args.option else 8
+    acct = LevelAccount(part["chunk"] // 64, off_bytes)
+    # The K steps run back to back between two barrier + device-synchronise brackets (the contract's
+    # timed region); every BFS is collective, so the ranks stay in step through its RCCL calls.
     ctx.synchronize()
     dist.barrier()
     w0 = time.perf_counter()
-    dev_ms = [g.dist_bfs(r, want_stats=False) for r in order[args.warmup:]]
+    dev_ms, order = [], []
+    for _ in range(args.steps):
+        for r in roots:
+            dev_ms.append(g.dist_bfs(r, want_stats=False))
+            order.append(r)
+            if rank == 0:
+                acct.add(g.level_stats(256))
     ctx.synchronize()
     wall_local = time.perf_counter() - w0
     dist.barrier()
     tt = torch.tensor([wall_local] + dev_ms, dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)  # max over ranks
     wall = float(tt[0])
-    dev_max = tt[1:].tolist()  # per root: the slowest rank's device time (source init -> last level)
-    steps_roots = order[args.warmup:]
-    m_total = float(sum(mcomp[r] for r in steps_roots))
-    value = m_total / wall / 1e9  # = harmonic mean of per-root TEPS when the roots share one component
+    dev_max = tt[1:].tolist()  # per BFS: the slowest rank's device time (source init -> last level)
+    m_total = float(sum(mcomp[r] for r in order))
+    value = hmean([mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(order, dev_max)])  # same basis as N = 1
     nnz = torch.tensor([g.nnz], dtype=torch.int64)
     dist.all_reduce(nnz)
     if rank == 0:
         out = common_fields(args, world, value, wall, part["nv_global"], g.m, int(nnz), len(roots),
                             f"1d-partition dp{world} (RCCL all-to-allv + all-gather + all-reduce in libbfsx)")
         out["scaling"] = "strong"
-        bu_bytes, bu_ms, bu_launches = 0, 0.0, 0
-        for ls in g.level_stats(256):  # rank 0, last timed BFS
-            if ls["direction"] == 2:
-                bu_bytes += level_bytes(ls, part["chunk"] // 64)
-                bu_ms += ls["kernel_ms"]
-                bu_launches += 1
-        out["roofline"] = roofline(bu_bytes, bu_ms, bu_launches,
-                                   "rank 0, last BFS; a bottom-up level's time includes its frontier all-gather")
-        out.update({"t_bfs_ms_mean": wall * 1e3 / max(len(steps_roots), 1),
-                    "t_bfs_dev_ms_max_mean": float(np.mean(dev_max)),
-                    "hmean_gteps_device": hmean([mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(steps_roots, dev_max)]),
-                    "m_comp_mean": float(np.mean([mcomp[r] for r in steps_roots])),
+        out["value_wall"] = m_total / wall / 1e9
+        out["roofline"] = acct.roofline("rank 0; a bottom-up level's time includes its frontier all-gather")
+        out["whole_bfs_roofline"] = dict(acct.whole(float(np.sum(dev_max)), len(dev_max)),
+                                         note="rank 0's level bytes over the max-over-ranks t_bfs")
+        out.update({"t_bfs_ms_mean": float(np.mean(dev_max)), "bfs_runs": len(dev_max),
+                    "m_comp_mean": float(np.mean([mcomp[r] for r in order])),
                     "graph_build_s": round(build_s, 3), "cpu_baseline": None,
                     "validation": {"roots": len(roots), "errors": val_errors,
                                    "rules": "Graph500 kernel-2 + BreadthFirstPaths.check, on device, collective"},

@@ -38,7 +38,7 @@ EXPORTS = [
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
     "bfsx_dist_begin", "bfsx_dist_frontier_info", "bfsx_dist_td_expand", "bfsx_dist_td_claim",
     "bfsx_dist_frontier_slice", "bfsx_dist_bu_step", "bfsx_dist_level_end", "bfsx_dist_finish",
-    "bfsx_dist_mcomp", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group", "bfsx_dist_bfs",
+    "bfsx_dist_mcomp", "bfsx_last_bfs_ms", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group", "bfsx_dist_bfs",
 ]
 COMM_ID_BYTES = 128
 
@@ -46,12 +46,12 @@ COMM_ID_BYTES = 128
 class Stats(C.Structure):
     _fields_ = [
         ("levels", C.c_int32), ("topdown_levels", C.c_int32), ("bottomup_levels", C.c_int32),
-        ("reserved0", C.c_int32), ("reached", C.c_int64), ("m_comp", C.c_int64),
+        ("persist_retries", C.c_int32), ("reached", C.c_int64), ("m_comp", C.c_int64),
         ("edges_examined", C.c_int64), ("t_bfs_ms", C.c_double), ("t_total_ms", C.c_double),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class LevelStat(C.Structure):
@@ -105,6 +105,7 @@ def lib():
         L.bfsx_result.argtypes = [_VP, _VP, _VP]
         L.bfsx_level_times.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
+        L.bfsx_last_bfs_ms.argtypes = [_VP, C.POINTER(C.c_double)]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
         L.bfsx_device_synchronize.argtypes = [_VP]
         I64P = C.POINTER(C.c_int64)
@@ -295,15 +296,19 @@ class Graph:
 
     def bfs_device_only(self, source):
         """The timed hot path: results stay on the device, no stats reduction.
-        Returns the device time (ms) of source init -> last level (hipEvents)."""
+        Returns the device time (ms) of source init -> last level complete (hipEvents)."""
         _check(lib().bfsx_bfs(self._h, source, None, None, None))
-        buf = np.empty(1 << 16, np.float64)
-        n = lib().bfsx_level_times(self._h, _p(buf), len(buf))
-        return float(buf[n - 1]) if n > 0 else float("nan")
+        return self.last_bfs_ms()
 
-    def result(self):
+    def last_bfs_ms(self):
+        """Device time (ms) of the most recent BFS of this graph (bfsx_last_bfs_ms)."""
+        ms = C.c_double()
+        _check(lib().bfsx_last_bfs_ms(self._h, C.byref(ms)))
+        return ms.value
+
+    def result(self, want_parent=True):
         dist = np.empty(self.nv, np.int32)
-        parent = np.empty(self.nv, np.int64)
+        parent = np.empty(self.nv, np.int64) if want_parent else None
         _check(lib().bfsx_result(self._h, _p(dist), _p(parent)))
         return dist, parent
 
@@ -389,9 +394,7 @@ class Graph:
             _check(lib().bfsx_dist_bfs(self._h, source, C.byref(st)))
             return st.as_dict()
         _check(lib().bfsx_dist_bfs(self._h, source, None))
-        buf = np.empty(1 << 16, np.float64)
-        n = lib().bfsx_level_times(self._h, _p(buf), len(buf))
-        return float(buf[n - 1]) if n > 0 else float("nan")
+        return self.last_bfs_ms()
 
     def dist_mcomp(self):
         a, b = C.c_int64(), C.c_int64()

@@ -269,6 +269,17 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         }
         return as_int(ctx->opt.persist_blocks);
     }
+    if (k == "persist_abort_at") {
+        if (v == "off") {
+            ctx->opt.persist_abort_at = -1;
+            return BFSX_OK;
+        }
+        char *end = nullptr;
+        const long x = strtol(value, &end, 10);
+        if (!end || *end || x < 0 || x > (1L << 20)) return fail(BFSX_E_ARG, "persist_abort_at must be off|level >= 0");
+        ctx->opt.persist_abort_at = (int)x;
+        return BFSX_OK;
+    }
     if (k == "slot_pairs") {
         char *end = nullptr;
         const long long x = strtoll(value, &end, 10);
@@ -671,8 +682,10 @@ int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_o
     const auto t0 = std::chrono::steady_clock::now();
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     bfsx_stats local{};
+    const int64_t retries0 = bfs_persist_fallbacks(g);
     int rc = bfs_run(g, source, &local);
     if (rc) return rc;
+    local.persist_retries = (int32_t)(bfs_persist_fallbacks(g) - retries0);
     if (dist_out || parent_out) {
         rc = bfs_copy_result(g, dist_out, parent_out);
         if (rc) return rc;
@@ -730,6 +743,13 @@ int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap) {
     int n = (int)std::min<size_t>(g->level_cum_ms.size(), (size_t)std::max(cap, 0));
     for (int i = 0; i < n; i++) cum_ms[i] = g->level_cum_ms[i];
     return n;
+}
+
+int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms) {
+    if (!g || !ms) return fail(BFSX_E_ARG, "bad argument");
+    if (g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
+    *ms = g->last_t_bfs_ms;
+    return BFSX_OK;
 }
 
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap) {

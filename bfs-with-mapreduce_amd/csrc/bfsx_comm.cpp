@@ -20,6 +20,7 @@
 #include <mutex>
 
 #include "bfsx_internal.h"
+#include "exchange_plan.h"
 
 namespace bfsx {
 
@@ -53,12 +54,12 @@ class RcclComm final : public Comm {
     }
     int alltoallv(const unsigned long long *d_send, const int64_t *scount, const int64_t *sdispl, unsigned long long *d_recv,
                   const int64_t *rcount, const int64_t *rdispl, hipStream_t st) override {
+        std::vector<P2pOp> ops;
+        alltoallv_ops(nranks, scount, sdispl, rcount, rdispl, ops);
         BFSX_NCCL_TRY(ncclGroupStart());
-        for (int p = 0; p < nranks; p++) {
-            if (scount[p] > 0)
-                BFSX_NCCL_TRY(ncclSend(d_send + sdispl[p], (size_t)scount[p], ncclUint64, p, comm, st));
-            if (rcount[p] > 0)
-                BFSX_NCCL_TRY(ncclRecv(d_recv + rdispl[p], (size_t)rcount[p], ncclUint64, p, comm, st));
+        for (const P2pOp &o : ops) {
+            if (o.send) BFSX_NCCL_TRY(ncclSend(d_send + o.offset, (size_t)o.count, ncclUint64, o.peer, comm, st));
+            else BFSX_NCCL_TRY(ncclRecv(d_recv + o.offset, (size_t)o.count, ncclUint64, o.peer, comm, st));
         }
         BFSX_NCCL_TRY(ncclGroupEnd());
         return BFSX_OK;

@@ -38,6 +38,7 @@ struct Options {
     int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
+    int persist_abort_at = -1;  // test hook: K3p aborts at this level of its launch (-1: never)
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------
@@ -78,6 +79,7 @@ int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t 
 struct BfsWorkspace;
 int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
+int64_t bfs_persist_fallbacks(const bfsx_graph *g); // BFS runs re-run without K3p after a barrier abort
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
 // multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
@@ -122,6 +124,7 @@ struct bfsx_graph {
     bfsx::BfsWorkspace *ws = nullptr;
     // most recent BFS
     int64_t last_source = -1;
+    double last_t_bfs_ms = 0.0; // device time of the most recent BFS (source init -> finalize)
     std::vector<double> level_cum_ms;
     std::vector<int32_t> level_dirs;
     std::vector<bfsx_level_stat> level_stats;

@@ -23,6 +23,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "bfsx_internal.h"
+#include "exchange_plan.h"
 
 namespace bfsx {
 
@@ -107,6 +108,8 @@ struct BfsWorkspace {
     size_t persist_lds = 0;     // dynamic LDS per workgroup (keeps one workgroup per CU)
     u64 persist_bar = 0;        // barrier rounds completed on persist_ctl
     bool persist_reset = true;  // persist_ctl must be zeroed before the next launch
+    bool persist_off = false;   // K3p cannot run on this device (occupancy check failed)
+    int64_t persist_fallbacks = 0; // BFS runs re-run without K3p after a barrier abort
     double clock_khz = 100000.0; // device wall-clock rate
     u64 pub_seq = 0;
     u64 *d_cursor = nullptr;            // bitmap -> queue compaction cursor
@@ -314,8 +317,8 @@ struct Part {
 constexpr int kRCap = 2048;
 struct RemoteQueue {
     u64 buf[kRCap];
+    u64 gbase; // 64-bit: a forced top-down level at scale 30 can route more than 2^32 pairs
     uint32_t n;
-    uint32_t gbase;
 };
 
 __device__ inline void rq_push(RemoteQueue &q, bool send, u64 pair) {
@@ -332,9 +335,9 @@ __device__ inline void rq_push(RemoteQueue &q, bool send, u64 pair) {
 __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
     const uint32_t n = q.n;
     if (n == 0) return;
-    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(pt.remote_tail, (u64)n);
+    if (threadIdx.x == 0) q.gbase = atomicAdd(pt.remote_tail, (u64)n);
     __syncthreads();
-    const uint32_t gb = q.gbase;
+    const u64 gb = q.gbase;
     for (uint32_t i = threadIdx.x; i < n; i += kBS) pt.remote[gb + i] = q.buf[i];
     __syncthreads();
     if (threadIdx.x == 0) q.n = 0;
@@ -628,7 +631,8 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
-                                                    PersistOut *out, uint32_t t_hub, int64_t bu_floor) {
+                                                    PersistOut *out, uint32_t t_hub, int64_t bu_floor,
+                                                    int inject_abort) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_scan[kBS + 1];
@@ -751,6 +755,15 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             }
             __syncthreads();
         }
+        // test hook (option "persist_abort_at"): every workgroup takes the abort path at this level, as a
+        // grid-barrier timeout would, and the host re-runs the BFS without K3p
+        if (it == inject_abort) {
+            if (b == 0 && tid == 0) {
+                out->abort = 1;
+                out->levels = (u64)it;
+            }
+            return;
+        }
         // this workgroup's level record
         {
             const u64 v0 = wave_sum(acc_mf), v1 = wave_sum(scanned), v2 = wave_sum(attempts), v3 = wave_max(acc_dmax),
@@ -853,10 +866,10 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
 
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
 template <class OffT>
-__global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pairs, uint32_t npairs,
+__global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pairs, u64 npairs,
                                                       const OffT *__restrict__ row_off, u64 *vis,
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
-                                                      LevelSlot *ring, int level, uint32_t lo, uint32_t slot) {
+                                                      LevelSlot *ring, int level, uint32_t lo, u64 slot) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ BlockQueue q;
     bq_init(q);
@@ -864,15 +877,15 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     const int32_t nd = level + 1;
     u64 acc_mf = 0, attempts = 0, acc_dmax = 0;
     // slot > 0: npairs = P * slot entries in P fixed slots of [count, slot pairs] (small levels)
-    for (uint32_t i0 = blockIdx.x * kBS; i0 < npairs; i0 += gridDim.x * kBS) {
-        const uint32_t i = i0 + threadIdx.x;
+    for (u64 i0 = (u64)blockIdx.x * kBS; i0 < npairs; i0 += (u64)gridDim.x * kBS) {
+        const u64 i = i0 + threadIdx.x;
         bool win = false;
         uint32_t vl = 0;
         bool have = i < npairs;
-        size_t at = i;
+        u64 at = i;
         if (have && slot) {
-            const uint32_t p = i / slot, k = i - p * slot;
-            const size_t base = (size_t)p * (slot + 1);
+            const u64 p = i / slot, k = i - p * slot;
+            const u64 base = p * (slot + 1);
             have = k < pairs[base];
             at = base + 1 + k;
         }
@@ -922,18 +935,18 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pa
 // Small top-down levels: pairs go to fixed per-destination slots of [count, cap pairs], so the exchange
 // needs no count all-to-all (and no host round trip) before the pairs move.
 __global__ __launch_bounds__(kBS) void k_bucket_slots(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
-                                                      uint32_t chunk, uint32_t cap, u64 *__restrict__ dcursor,
+                                                      uint32_t chunk, u64 cap, u64 *__restrict__ dcursor,
                                                       u64 *__restrict__ out) {
     const uint64_t n = *d_n;
     for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS) {
         const u64 pr = pairs[i];
         const uint32_t d = (uint32_t)(pr >> 32) / chunk;
         const u64 r = atomicAdd(&dcursor[d], 1ull);
-        out[(size_t)d * (cap + 1) + 1 + r] = pr;
+        out[(u64)d * (cap + 1) + 1 + r] = pr;
     }
 }
-__global__ void k_slot_headers(const u64 *__restrict__ dcursor, int nranks, uint32_t cap, u64 *__restrict__ out) {
-    for (int p = threadIdx.x; p < nranks; p += blockDim.x) out[(size_t)p * (cap + 1)] = dcursor[p];
+__global__ void k_slot_headers(const u64 *__restrict__ dcursor, int nranks, u64 cap, u64 *__restrict__ out) {
+    for (int p = threadIdx.x; p < nranks; p += blockDim.x) out[(u64)p * (cap + 1)] = dcursor[p];
 }
 
 __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
@@ -1528,17 +1541,34 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     size_t mfree = 0, mtotal = 0;
     BFSX_HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
     if ((size_t)g->nnz * 4 + nr * 20 > mfree / 2) return BFSX_OK;
-    BFSX_HIP_TRY(hipMalloc(&keys.p, nr * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&keys2.p, nr * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ids.p, nr * sizeof(uint32_t)));
-    BFSX_HIP_TRY(hipMalloc(&ids2.p, nr * sizeof(uint32_t)));
+    // from here on an allocation failure (e.g. ranks of an in-process group racing for one device's
+    // memory) leaves the domain off instead of failing the BFS: it is an optimisation of the pull
+    // kernel only, and top1 is encoded last, after every allocation has succeeded
+#define HUB_ALLOC(call)                                                                          \
+    do {                                                                                         \
+        const hipError_t h_ = (call);                                                            \
+        if (h_ == hipErrorOutOfMemory) {                                                         \
+            (void)hipGetLastError();                                                             \
+            for (void **p_ : {(void **)&ws->hub_id, (void **)&ws->colh, (void **)&ws->hfront})   \
+                if (*p_) {                                                                       \
+                    (void)hipFree(*p_);                                                          \
+                    *p_ = nullptr;                                                               \
+                }                                                                                \
+            return BFSX_OK;                                                                      \
+        }                                                                                        \
+        BFSX_HIP_TRY(h_);                                                                        \
+    } while (0)
+    HUB_ALLOC(hipMalloc(&keys.p, nr * sizeof(uint32_t)));
+    HUB_ALLOC(hipMalloc(&keys2.p, nr * sizeof(uint32_t)));
+    HUB_ALLOC(hipMalloc(&ids.p, nr * sizeof(uint32_t)));
+    HUB_ALLOC(hipMalloc(&ids2.p, nr * sizeof(uint32_t)));
     hipLaunchKernelGGL(k_hub_keys, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)degs.p, ng, (uint32_t *)keys.p,
                        (uint32_t *)ids.p);
     BFSX_HIP_TRY(hipGetLastError());
     size_t tb = 0;
     BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
                                            (uint32_t *)ids2.p, nr, 0, 32, st));
-    BFSX_HIP_TRY(hipMalloc(&sort_tmp.p, std::max<size_t>(tb, 16)));
+    HUB_ALLOC(hipMalloc(&sort_tmp.p, std::max<size_t>(tb, 16)));
     BFSX_HIP_TRY(rocprim::radix_sort_pairs(sort_tmp.p, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
                                            (uint32_t *)ids2.p, nr, 0, 32, st));
     // the hub set is closed under degree ties: every vertex of degree >= the k-th largest degree (so a
@@ -1553,22 +1583,23 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     BFSX_HIP_TRY(hipMemcpyAsync(&keff, ws->d_red, sizeof(keff), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     k = (int64_t)keff;
+    HUB_ALLOC(hipMalloc(&ws->hub_id, (size_t)k * sizeof(uint32_t)));
+    HUB_ALLOC(hipMalloc(&hidx.p, nr * sizeof(uint32_t)));
+    HUB_ALLOC(hipMalloc(&ws->colh, (size_t)std::max<int64_t>(g->nnz, 1) * sizeof(uint32_t)));
+    HUB_ALLOC(hipMalloc(&ws->hfront, (size_t)((k + 63) / 64) * sizeof(u64)));
+#undef HUB_ALLOC
     ws->hub_tdeg = ~kth;
-    BFSX_HIP_TRY(hipMalloc(&ws->hub_id, (size_t)k * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMemcpyAsync(ws->hub_id, ids2.p, (size_t)k * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    BFSX_HIP_TRY(hipMalloc(&hidx.p, nr * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMemsetAsync(hidx.p, 0xFF, nr * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_hub_index, dim3(clamp_grid((k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->hub_id, k,
                        (uint32_t *)hidx.p);
     BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipMalloc(&ws->colh, (size_t)std::max<int64_t>(g->nnz, 1) * sizeof(uint32_t)));
     hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid((g->nnz + kBS - 1) / kBS, 65536)), dim3(kBS), 0, st, g->d_col,
                        g->nnz, (const uint32_t *)hidx.p, 0u, ws->colh);
     BFSX_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
                        ws->top1, g->nv, (const uint32_t *)hidx.p, ws->top1_flag, ws->top1);
     BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipMalloc(&ws->hfront, (size_t)((k + 63) / 64) * sizeof(u64)));
     BFSX_HIP_TRY(hipStreamSynchronize(st)); // the temporaries are freed on return
     ws->hub_k = k;
     return BFSX_OK;
@@ -1792,12 +1823,16 @@ int persist_blocks(const bfsx_ctx *ctx) {
 }
 
 // Whether a top-down level of nf vertices (largest degree dmax, < 0: unknown) may start K3p: every
-// workgroup's slice must fit its output segment whatever it discovers.
-bool persist_fits(const bfsx_ctx *ctx, int64_t nf, int64_t dmax) {
-    if (!ctx->opt.persist || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
-    const int64_t G = persist_blocks(ctx);
+// workgroup's slice must fit its output segment whatever it discovers.  G is the grid the launch will
+// use: fixed at the graph's first K3p launch (ws->persist_grid), the option's value before it.
+bool persist_fits(const bfsx_ctx *ctx, const BfsWorkspace *ws, int64_t nf, int64_t dmax) {
+    if (!ctx->opt.persist || ws->persist_off || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
+    const int64_t G = ws->persist_seg ? ws->persist_grid : persist_blocks(ctx);
+    if (G < 1) return false;
     return ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
 }
+
+constexpr int kPersistAborted = -1000; // internal: K3p aborted (barrier timeout); bfs_run retries without it
 
 // Run K3p from `level` (frontier of nf vertices in ws->qa; its last frontier lands in ws->qb).
 // Returns the number of levels it ran (>= 1) with their records in the PersistOut, or an error.
@@ -1830,6 +1865,16 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                 ws->persist_lds = dyn;
             (void)hipGetLastError();
         }
+        // the grid barrier needs every workgroup resident at once: never launch more than the occupancy
+        // API says fit (one per CU with the LDS padding above)
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBS, ws->persist_lds) != hipSuccess) per_cu = 0;
+        (void)hipGetLastError();
+        ws->persist_grid = std::min(G, per_cu * g->ctx->num_cus);
+        if (ws->persist_grid < 1) {
+            ws->persist_off = true; // cannot be co-resident: narrow levels stay per-level launches
+            return 0;
+        }
     }
     if (ws->persist_reset) {
         BFSX_HIP_TRY(hipMemsetAsync(ws->persist_ctl, 0, sizeof(PersistCtl), st));
@@ -1847,19 +1892,20 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws));
+                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws), opt.persist_abort_at);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws));
+                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws), opt.persist_abort_at);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     std::atomic_thread_fence(std::memory_order_acquire);
     if (out->abort) {
         ws->persist_reset = true;
-        return fail(BFSX_E_HIP, "persistent top-down: grid barrier timed out or a segment overflowed");
+        set_error("persistent top-down: grid barrier timed out or a segment overflowed");
+        return kPersistAborted;
     }
     if (out->levels < 1 || out->levels > (u64)kPersistLevels) {
         ws->persist_reset = true;
@@ -1892,7 +1938,30 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     delete ws;
 }
 
+namespace {
+
+int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist);
+
+} // namespace
+
+// K3p's grid barrier needs all of its workgroups resident; the launch is sized by the occupancy API,
+// but another context on the same device can still hold CUs.  A barrier that times out aborts the
+// launch (every workgroup exits), and the BFS is re-run from its source without K3p -- the level
+// loop is deterministic, so the result is the same.
 int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
+    int rc = bfs_run_impl(g, source, stats, true);
+    if (rc == kPersistAborted) {
+        g->ws->persist_fallbacks++;
+        rc = bfs_run_impl(g, source, stats, false);
+    }
+    return rc == kPersistAborted ? fail(BFSX_E_HIP, "persistent top-down aborted twice") : rc;
+}
+
+int64_t bfs_persist_fallbacks(const bfsx_graph *g) { return g->ws ? g->ws->persist_fallbacks : 0; }
+
+namespace {
+
+int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist) {
     if (source < 0 || source >= g->nv)
         return fail(BFSX_E_RANGE, "source vertex " + std::to_string(source) + " outside [0, " +
                                       std::to_string(g->nv) + ")");
@@ -2030,40 +2099,43 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             in_queue = true;
         }
         snapped = false;
-        if (dir == BFSX_DIR_TOPDOWN && persist_fits(ctx, nf, dmax)) {
+        if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(ctx, ws, nf, dmax)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
             const int ran = persist_td(g, ws, level, nf, mu);
             if (ran < 0) return ran;
-            const PersistOut &po = *reinterpret_cast<const PersistOut *>(ws->h_pout);
-            for (int i = 0; i < ran; i++) {
-                const PersistRec &r = po.rec[i];
-                bfsx_level_stat ls{};
-                ls.direction = BFSX_DIR_TOPDOWN;
-                ls.level = level + i;
-                ls.frontier_in = nf;
-                ls.frontier_out = (int64_t)r.qtail;
-                ls.mf_in = (int64_t)r.scanned;
-                ls.unvisited_in = nv - visited - ws->n_dead;
-                ls.scanned = (int64_t)r.scanned;
-                ls.claims = (int64_t)r.claims;
-                g->level_stats.push_back(ls);
-                g->level_dirs.push_back(BFSX_DIR_TOPDOWN);
-                timing.push_back({level, true, (double)(r.t_end - po.t0) / ws->clock_khz,
-                                  (double)(r.t_end - (i ? po.rec[i - 1].t_end : po.t0)) / ws->clock_khz});
-                examined += ls.scanned;
-                visited += ls.frontier_out;
-                mu -= (int64_t)r.mf;
-                prev_nf = nf;
-                nf = ls.frontier_out;
-                mf = (int64_t)r.mf;
-                dmax = (int64_t)r.dmax;
-                mfh = ws->hub_k > 0 ? (int64_t)r.mfh : -1;
+            // ran == 0: K3p unavailable on this device (occupancy check): per-level launches below
+            if (ran > 0) {
+                const PersistOut &po = *reinterpret_cast<const PersistOut *>(ws->h_pout);
+                for (int i = 0; i < ran; i++) {
+                    const PersistRec &r = po.rec[i];
+                    bfsx_level_stat ls{};
+                    ls.direction = BFSX_DIR_TOPDOWN;
+                    ls.level = level + i;
+                    ls.frontier_in = nf;
+                    ls.frontier_out = (int64_t)r.qtail;
+                    ls.mf_in = (int64_t)r.scanned;
+                    ls.unvisited_in = nv - visited - ws->n_dead;
+                    ls.scanned = (int64_t)r.scanned;
+                    ls.claims = (int64_t)r.claims;
+                    g->level_stats.push_back(ls);
+                    g->level_dirs.push_back(BFSX_DIR_TOPDOWN);
+                    timing.push_back({level, true, (double)(r.t_end - po.t0) / ws->clock_khz,
+                                      (double)(r.t_end - (i ? po.rec[i - 1].t_end : po.t0)) / ws->clock_khz});
+                    examined += ls.scanned;
+                    visited += ls.frontier_out;
+                    mu -= (int64_t)r.mf;
+                    prev_nf = nf;
+                    nf = ls.frontier_out;
+                    mf = (int64_t)r.mf;
+                    dmax = (int64_t)r.dmax;
+                    mfh = ws->hub_k > 0 ? (int64_t)r.mfh : -1;
+                }
+                std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
+                td_levels += ran;
+                level += ran - 1;
+                if (nf == 0) break;
+                continue;
             }
-            std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
-            td_levels += ran;
-            level += ran - 1;
-            if (nf == 0) break;
-            continue;
         }
         if (dir == BFSX_DIR_TOPDOWN) {
             // a wide top-down level may hand over to bottom-up: snapshot the visited bitmap (8 B per 64
@@ -2151,6 +2223,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         g->level_stats[l].kernel_ms = k;
     }
     g->last_source = source;
+    g->last_t_bfs_ms = ms;
     if (stats) {
         stats->levels = levels;
         stats->topdown_levels = td_levels;
@@ -2160,6 +2233,8 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     }
     return BFSX_OK;
 }
+
+} // namespace
 
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached) {
     BfsWorkspace *ws = g->ws;
@@ -2350,11 +2425,11 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     const dim3 grid(clamp_grid((n + kBS - 1) / kBS, cap));
     if (ws->off32)
-        hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (uint32_t)n, ws->off32, ws->vis,
-                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, 0u);
+        hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, ws->off32, ws->vis,
+                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0);
     else
-        hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (uint32_t)n, g->d_row_off,
-                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, 0u);
+        hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
+                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -2432,6 +2507,11 @@ int dist_finish(bfsx_graph *g) {
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
+    {
+        float ms = 0.f;
+        BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
+        g->last_t_bfs_ms = ms;
+    }
     const int levels = ws->d_level;
     g->level_cum_ms.resize(levels);
     for (int l = 0; l < levels; l++) {
@@ -2533,7 +2613,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int64_t visited_local = (source >= g->v_lo && source < g->v_lo + g->nv) ? 1 : 0;
     bool snapped = false; // ws->front holds the visited slice from before the last (top-down) level
     int td_levels = 0, bu_levels = 0;
-    std::vector<int64_t> scount(P), sdispl(P), rcount(P), rdispl(P);
+    ExchangePlan plan;
     std::vector<u64> hc(2 * kMaxRanks);
     for (;;) {
         const int level = ws->d_level;
@@ -2593,15 +2673,12 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (int e = grow(ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
                 if (int e = grow(ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
                 hipLaunchKernelGGL(k_bucket_slots, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                                   (uint32_t)g->chunk, (uint32_t)slot, dcursor, ws->sendbuf);
+                                   (uint32_t)g->chunk, (u64)slot, dcursor, ws->sendbuf);
                 BFSX_HIP_TRY(hipGetLastError());
-                hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, st, dcursor, P, (uint32_t)slot, ws->sendbuf);
+                hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, st, dcursor, P, (u64)slot, ws->sendbuf);
                 BFSX_HIP_TRY(hipGetLastError());
-                for (int p = 0; p < P; p++) {
-                    scount[p] = rcount[p] = slot + 1;
-                    sdispl[p] = rdispl[p] = p * (slot + 1);
-                }
-                ro = P * slot;
+                plan_slots(P, slot, plan);
+                ro = P * slot; // candidate entries the claim kernel reads
             } else {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, P, dcount);
@@ -2613,30 +2690,23 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
                     return e;
                 if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
-                int64_t so = 0;
-                for (int p = 0; p < P; p++) {
-                    scount[p] = (int64_t)hc[p];
-                    rcount[p] = (int64_t)hc[P + p];
-                    sdispl[p] = so;
-                    rdispl[p] = ro;
-                    so += scount[p];
-                    ro += rcount[p];
-                }
+                plan_counted(P, hc.data(), hc.data() + P, plan);
+                ro = plan.recv_total;
                 if (int e = grow(ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
             }
-            if (int e = cm->alltoallv(ws->sendbuf, scount.data(), sdispl.data(), ws->recvbuf, rcount.data(),
-                                      rdispl.data(), st))
+            if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
+                                      plan.rcount.data(), plan.rdispl.data(), st))
                 return e;
             if (ro > 0) {
                 const dim3 grid(clamp_grid((ro + kBS - 1) / kBS, cap));
                 if (ws->off32)
-                    hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (uint32_t)ro,
+                    hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (uint32_t)slot);
+                                       (u64)slot);
                 else
-                    hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (uint32_t)ro,
+                    hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (uint32_t)slot);
+                                       (u64)slot);
                 BFSX_HIP_TRY(hipGetLastError());
             }
             td_levels++;

@@ -59,7 +59,7 @@ typedef struct bfsx_stats {
     int32_t levels;          /* map/reduce passes = eccentricity(source) + 1 */
     int32_t topdown_levels;  /* levels run as push (queue -> queue) */
     int32_t bottomup_levels; /* levels run as pull (bitmap -> bitmap) */
-    int32_t reserved0;
+    int32_t persist_retries; /* times this BFS was re-run without the persistent push kernel (barrier abort) */
     int64_t reached;         /* vertices with finite distance (BLACK at the end) */
     int64_t m_comp;          /* input edge tuples inside the source's component (TEPS numerator) */
     int64_t edges_examined;  /* sum of frontier degrees over top-down levels + probes (approximate) */
@@ -97,7 +97,10 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
  *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS)
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
- *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU; fixed at a graph's first BFS)
+ *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU, capped by the occupancy API so
+ *                 that every workgroup is resident; fixed at a graph's first BFS)
+ *   "persist_abort_at" = int|off (test hook: that persistent launch aborts at its k-th level as a barrier
+ *                 timeout would; the BFS is then re-run without it; default off)
  *   "hub_bits" = auto|off|1..30 (bottom-up probes of the 2^b highest-degree vertices go to a small
  *                 gathered bitmap; auto = n/1024 rounded up to a power of two; fixed at a graph's first BFS)
  *   "hybrid" = auto|off|force (a top-down level whose frontier's edges sit mostly in hub-domain vertices
@@ -158,6 +161,9 @@ int bfsx_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
 /* Device time of each level of the most recent bfsx_bfs, cumulative like the reference's
  * Stopwatch (BfsSpark.java:59,63,111-112).  Returns the number of levels written (<= cap). */
 int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap);
+/* Device time (ms) of the most recent BFS of g: source init -> last level complete, the stats.t_bfs_ms
+ * figure without the m_comp reduction bfsx_bfs performs when stats are requested (benchmark loops). */
+int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms);
 /* Per-level direction of the most recent bfsx_bfs (BFSX_DIR_TOPDOWN / BFSX_DIR_BOTTOMUP). */
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap);
 

@@ -25,7 +25,27 @@ def test_bottom_up_level_bytes(bench):
 
 def test_top_down_level_bytes(bench):
     ls = {"direction": 1, "frontier_in": 10, "mf_in": 300, "frontier_out": 20}
-    assert bench.level_bytes(ls, 1) == 20 * 10 + 4 * 300 + 28 * 20
+    # uint32 row offsets (the default below 2^32 adjacency entries), then int64 offsets
+    assert bench.level_bytes(ls, 1) == 12 * 10 + 4 * 300 + 20 * 20
+    assert bench.level_bytes(ls, 1, off_bytes=8) == 20 * 10 + 4 * 300 + 28 * 20
+
+
+def test_hybrid_level_bytes(bench):
+    ls = {"direction": 3, "unvisited_in": 1000, "scanned": 300, "frontier_out": 20}
+    assert bench.level_bytes(ls, 64) == 16 * 64 + 4 * 1000 + 4 * 300 + 8 * 20
+
+
+def test_level_account_whole_bfs(bench):
+    acct = bench.LevelAccount(64, 4)
+    bu = {"direction": 2, "unvisited_in": 1000, "stage2": 100, "claims": 10, "walked": 50, "frontier_out": 600,
+          "kernel_ms": 0.5}
+    td = {"direction": 1, "frontier_in": 10, "mf_in": 300, "frontier_out": 20, "kernel_ms": 0.1}
+    acct.add([td, bu])
+    assert acct.bu_launches == 1 and acct.bu_bytes == bench.level_bytes(bu, 64)
+    assert acct.all_bytes == bench.level_bytes(bu, 64) + bench.level_bytes(td, 64)
+    w = acct.whole(2.0, 1)  # 2 ms for one BFS
+    assert abs(w["achieved"] - round(acct.all_bytes / 2e-3 / 1e9, 1)) < 1e-9
+    assert bench.edge_scan_equivalent(1 << 20, 1 << 16, 1.0)["frac_of_peak"] > 0
 
 
 def test_hmean(bench):

@@ -1,0 +1,130 @@
+"""largeG (BASELINE configs[2]) on the GPU.
+
+largeG.txt is listed in the reference's .MISSING_LARGE_BLOBS (not in the checkout), so:
+
+1. test_largeg_known_answers runs whenever the file is supplied -- $BFSX_LARGEG, tests/golden/largeG.txt
+   or test-sets/largeG.txt -- and otherwise skips.  It checks every known answer the reference's own files
+   hold for it:
+     - algs4.jar!/BreadthFirstPaths.java:27-34: d(0..6) = 0, 418, 323, 168, 144, 566, 349 from source 0,
+       and the shortest-path prefixes printed there (the k-th vertex of a shortest path is at distance
+       k, and consecutive vertices are joined by an edge);
+     - algs4.jar!/CC.java:20-22: one connected component (every vertex reached);
+     - algs4.jar!/Cycle.java:14-15: the edges of the cycle 996673-762-840164-4619-785187-194717-996673;
+     - PDF p.5 section 1.5: 15,172,126 directed adjacency entries (V = 1,000,000);
+   plus the full distance vector bit-exact against the oracle on the same file.  Beyond these the
+   file's result is "parity unpinned" (no reference output for it exists).
+2. test_largeg_standin runs always: a graph of largeG's size and shape class (1,000,000 vertices,
+   7,586,063 edges, a random geometric graph with hundreds of levels), written as an algs4 file and driven
+   through the whole path (GPU tokenizer -> CSR -> BFS from 0), bit-exact against the oracle, with the
+   per-level latency recorded (the config is latency-bound: ~560 levels of ~2,000-vertex frontiers).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+INF = 2147483647
+
+# algs4.jar!/BreadthFirstPaths.java:27-34 (source 0)
+LARGEG_DIST = {0: 0, 1: 418, 2: 323, 3: 168, 4: 144, 5: 566, 6: 349}
+LARGEG_PATH_PREFIXES = [
+    [0, 932942, 474885, 82707, 879889, 971961],  # 0 -> 1, 5, 6
+    [0, 460790, 53370, 594358, 780059, 287921],  # 0 -> 2
+    [0, 713461, 75230, 953125, 568284, 350405],  # 0 -> 3
+    [0, 460790, 53370, 310931, 440226, 380102],  # 0 -> 4
+]
+# algs4.jar!/Cycle.java:14-15
+LARGEG_CYCLE = [996673, 762, 840164, 4619, 785187, 194717, 996673]
+
+
+def find_largeg():
+    for p in (os.environ.get("BFSX_LARGEG", ""), os.path.join(GOLDEN, "largeG.txt"),
+              os.path.join(ROOT, "test-sets", "largeG.txt")):
+        if p and os.path.isfile(p):
+            return p
+    return None
+
+
+def has_edge(off, col, a, b):
+    return b in col[off[a]:off[a + 1]]
+
+
+def test_largeg_known_answers(ctx):
+    path = find_largeg()
+    if path is None:
+        pytest.skip("largeG.txt not supplied (reference .MISSING_LARGE_BLOBS:1); set BFSX_LARGEG to run")
+    with ctx.load_algs4(path) as g:
+        nv_g = g.nv
+        assert nv_g == 1_000_000
+        assert g.nnz == 15_172_126  # PDF p.5: directed entries, no duplicates or self-loops
+        dist, parent, st = g.bfs(0)
+        off, col = g.csr()
+    for v, d in LARGEG_DIST.items():
+        assert dist[v] == d, (v, dist[v], d)
+    assert st["reached"] == nv_g
+    assert int((dist == INF).sum()) == 0  # CC.java:20-22: one component
+    assert st["levels"] == int(dist.max()) + 1 and dist.max() >= 566
+    for pre in LARGEG_PATH_PREFIXES:
+        for k, x in enumerate(pre):
+            assert dist[x] == k
+        for a, b in zip(pre, pre[1:]):
+            assert has_edge(off, col, a, b)
+    for a, b in zip(LARGEG_CYCLE, LARGEG_CYCLE[1:]):
+        assert has_edge(off, col, a, b) and has_edge(off, col, b, a)
+    nv, u, v = O.load_graphfileutil(path)
+    ooff, ocol = O.build_sets(nv, u, v)
+    ref, _ = O.csr_bfs(nv, ooff, ocol, 0)
+    assert np.array_equal(dist, ref)
+    assert O.validate(nv, ooff, ocol, 0, dist, parent) == 0
+
+
+def write_standin(path, side=1000, m=7_586_063, radius=2, seed=2026):
+    """largeG-class algs4 file: vertices on a side x side grid (id = y*side + x); every edge joins a random
+    vertex to a random vertex at most `radius` cells away on each axis (diameter ~ side/radius)."""
+    rng = np.random.default_rng(seed)
+    nv = side * side
+    a = rng.integers(0, nv, m)
+    dx = rng.integers(-radius, radius + 1, m)
+    dy = rng.integers(-radius, radius + 1, m)
+    x = np.clip(a % side + dx, 0, side - 1)
+    y = np.clip(a // side + dy, 0, side - 1)
+    b = y * side + x
+    with open(path, "w") as f:
+        f.write(f"{nv}\n{m}\n")
+        lines = np.char.add(np.char.add(a.astype(str), " "), b.astype(str))
+        f.write("\n".join(lines.tolist()))
+        f.write("\n")
+    return nv, m
+
+
+def test_largeg_standin(ctx, tmp_path):
+    path = str(tmp_path / "largeG_like.txt")
+    nv, m = write_standin(path)
+    onv, u, v = O.load_graphfileutil(path)
+    assert onv == nv and len(u) == m
+    off, col = O.build_sets(nv, u, v)
+    ref, _ = O.csr_bfs(nv, off, col, 0)
+    with ctx.load_algs4(path) as g:
+        assert g.nv == nv and g.m == m and g.nnz == off[-1]
+        g.bfs(0)  # warm-up
+        dist, parent, st = g.bfs(0)
+        levels = g.level_stats(4096)
+    assert np.array_equal(dist, ref)
+    assert O.validate(nv, off, col, 0, dist, parent) == 0
+    assert st["levels"] == int(ref[ref != INF].max()) + 1 and st["levels"] > 300
+    assert st["m_comp"] == O.mcomp(u, v, ref)
+    rec = {"config": "largeG stand-in (1e6 vertices, 7,586,063 edges, geometric)", "levels": st["levels"],
+           "t_bfs_ms": round(st["t_bfs_ms"], 3), "us_per_level": round(st["t_bfs_ms"] * 1e3 / st["levels"], 2),
+           "topdown_levels": st["topdown_levels"], "bottomup_levels": st["bottomup_levels"],
+           "mteps": round(st["m_comp"] / (st["t_bfs_ms"] * 1e-3) / 1e6, 1),
+           "frontier_mean": round(float(np.mean([l["frontier_in"] for l in levels])), 1)}
+    print(json.dumps(rec))
+    out = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "largeg_standin_test.json"), "w") as f:
+            json.dump(rec, f)

@@ -240,6 +240,62 @@ def test_persistent_topdown_matches_per_level_kernels(ctx, case, blocks):
         assert res["on", src] == res["off", src]
 
 
+@pytest.mark.parametrize("abort_at", [0, 3])
+def test_persistent_abort_falls_back(ctx, abort_at):
+    """A K3p launch whose grid barrier gives up (here: the "persist_abort_at" hook, the same exit path a
+    barrier timeout takes when another context holds CUs) makes every workgroup exit; the BFS is re-run
+    without K3p and still returns the oracle's distances (no random failures from co-residency)."""
+    nv = 3000
+    u, v = np.arange(nv - 1, dtype=np.uint32), np.arange(1, nv, dtype=np.uint32)  # one long K3p launch
+    off, col = O.build_sets(nv, u, v)
+    ref, _ = O.csr_bfs(nv, off, col, 0)
+    try:
+        ctx.set_option("persist_abort_at", str(abort_at))
+        with ctx.from_edges(nv, u, v) as g:
+            for _ in range(2):  # the barrier counters are reset after an abort
+                d, p, st = g.bfs(0)
+                assert st["persist_retries"] == 1
+                assert np.array_equal(d, ref)
+                assert O.validate(nv, off, col, 0, d, p) == 0
+                assert st["levels"] == nv
+        ctx.set_option("persist_abort_at", "off")
+        with ctx.from_edges(nv, u, v) as g:
+            d, _, st = g.bfs(0)
+            assert st["persist_retries"] == 0 and np.array_equal(d, ref)
+    finally:
+        ctx.set_option("persist_abort_at", "off")
+
+
+def test_persist_blocks_changed_between_runs(ctx):
+    """persist_blocks raised after a graph's first K3p launch: the launch keeps the grid it was set up
+    with, and the entry bound (every slice fits its output segment) is checked against THAT grid."""
+    # root 0 -> 1000 children -> 40 leaves each: the second frontier (1000 vertices of degree 41) fits a
+    # 256-workgroup grid's segments (4 x 41 entries) but not a 2-workgroup grid's (500 x 40 discoveries)
+    kids, fan = 1000, 40
+    nv = 1 + kids + kids * fan
+    child = np.arange(1, kids + 1)
+    u = np.r_[np.zeros(kids), np.repeat(child, fan)].astype(np.uint32)
+    v = np.r_[child, np.arange(kids + 1, nv)].astype(np.uint32)
+    plen = kids
+    off, col = O.build_sets(nv, u, v)
+    ref, _ = O.csr_bfs(nv, off, col, 0)
+    try:
+        ctx.set_option("direction", "topdown")  # push levels only, so the wide level is a K3p candidate
+        ctx.set_option("persist_blocks", "2")
+        with ctx.from_edges(nv, u, v) as g:
+            d, _, st = g.bfs(0)
+            assert np.array_equal(d, ref)
+            ctx.set_option("persist_blocks", "auto")
+            for src in (0, plen - 2):
+                d, p, st = g.bfs(src)
+                r2, _ = O.csr_bfs(nv, off, col, src)
+                assert np.array_equal(d, r2) and st["persist_retries"] == 0
+                assert O.validate(nv, off, col, src, d, p) == 0
+    finally:
+        ctx.set_option("persist_blocks", "auto")
+        ctx.set_option("direction", "auto")
+
+
 @pytest.mark.parametrize("bits", ["auto", "64"])
 def test_offset_width_paths(ctx, bits):
     """uint32 and int64 row-offset instantiations of every traversal kernel agree with the oracle (int64
