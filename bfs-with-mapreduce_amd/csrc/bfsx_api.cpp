@@ -153,6 +153,30 @@ int load_algs4_device(bfsx_ctx *ctx, const char *path, int64_t &nv, int64_t &m, 
 }
 
 } // namespace
+
+// Original vertex id -> the internal id every device array is indexed by (identity without relabel).
+int to_internal(const bfsx_graph *g, int64_t v, int64_t *out) {
+    if (!g->d_perm) {
+        *out = v;
+        return BFSX_OK;
+    }
+    uint32_t x = 0;
+    BFSX_HIP_TRY(hipMemcpy(&x, g->d_perm + v, sizeof(x), hipMemcpyDeviceToHost));
+    *out = (int64_t)x;
+    return BFSX_OK;
+}
+
+int to_original(const bfsx_graph *g, int64_t x, int64_t *out) {
+    if (!g->d_inv || x < 0) {
+        *out = x;
+        return BFSX_OK;
+    }
+    uint32_t v = 0;
+    BFSX_HIP_TRY(hipMemcpy(&v, g->d_inv + x, sizeof(v), hipMemcpyDeviceToHost));
+    *out = (int64_t)v;
+    return BFSX_OK;
+}
+
 } // namespace bfsx
 
 using namespace bfsx;
@@ -252,6 +276,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         if (v == "degree") ctx->opt.degree_order = true;
         else if (v == "id") ctx->opt.degree_order = false;
         else return fail(BFSX_E_ARG, "row_order must be degree|id");
+        return BFSX_OK;
+    }
+    if (k == "relabel") {
+        if (v == "on") ctx->opt.relabel = true;
+        else if (v == "off") ctx->opt.relabel = false;
+        else return fail(BFSX_E_ARG, "relabel must be on|off");
         return BFSX_OK;
     }
     if (k == "alpha") return as_int(ctx->opt.alpha);
@@ -355,13 +385,15 @@ static bfsx_graph *new_partition(bfsx_ctx *ctx, int64_t nv, int64_t m, int rank,
     return g;
 }
 
+// dist: built for the partitioned loop (bfsx_dist_*), which runs on original ids even at one rank (the
+// relabel is a single-device layout; a partition would hand every hub to rank 0)
 static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m, int rank,
-                                   int nranks, bfsx_graph **out) {
+                                   int nranks, bfsx_graph **out, bool dist) {
     bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
     if (!g) return fail(BFSX_E_OOM, "graph");
     set_build_chunk(ctx->opt.build_chunk);
-    int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, &g->d_row_off, &g->d_col,
-                              &g->nnz, &g->d_tuple_cnt, g->v_lo, nv);
+    int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, ctx->opt.relabel && !dist,
+                              &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt, &g->d_perm, &g->d_inv, g->v_lo, nv);
     if (rc) {
         delete g;
         return rc;
@@ -371,7 +403,7 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
 }
 
 static int graph_from_host_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
-                                 int rank, int nranks, bfsx_graph **out) {
+                                 int rank, int nranks, bfsx_graph **out, bool dist) {
     if (!ctx || !out || nv <= 0 || m < 0 || (m > 0 && (!u || !v))) return fail(BFSX_E_ARG, "bad argument");
     if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
     if (nv > (int64_t)INT32_MAX) return fail(BFSX_E_ARG, "nv must be < 2^31 on one device");
@@ -392,7 +424,7 @@ static int graph_from_host_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, c
             hipMemcpyAsync(d_v, v, m * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
             rc = fail(BFSX_E_HIP, "H2D tuples");
     }
-    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, rank, nranks, out);
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, rank, nranks, out, dist);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(d_u);
     (void)hipFree(d_v);
@@ -401,12 +433,12 @@ static int graph_from_host_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, c
 
 int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
                           bfsx_graph **out) {
-    return graph_from_host_edges(ctx, nv, u, v, m, 0, 1, out);
+    return graph_from_host_edges(ctx, nv, u, v, m, 0, 1, out, false);
 }
 
 int bfsx_dist_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m, int rank,
                                int nranks, bfsx_graph **out) {
-    return graph_from_host_edges(ctx, nv, u, v, m, rank, nranks, out);
+    return graph_from_host_edges(ctx, nv, u, v, m, rank, nranks, out, true);
 }
 
 int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
@@ -416,7 +448,7 @@ int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
     int rc = load_algs4_device(ctx, path, nv, m, d_u, d_v);
     if (rc) return rc;
     if (nv > (int64_t)INT32_MAX) rc = fail(BFSX_E_ARG, "nv must be < 2^31 on one device");
-    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, 0, 1, out);
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, 0, 1, out, false);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(d_u);
     (void)hipFree(d_v);
@@ -472,7 +504,7 @@ int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed
 }
 
 static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
-                           bfsx_graph **out) {
+                           bfsx_graph **out, bool dist) {
     if (!ctx || !out || scale < 1 || scale > 30 || edgefactor < 1) return fail(BFSX_E_ARG, "bad argument");
     if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
     BFSX_HIP_TRY(hipSetDevice(ctx->device));
@@ -482,8 +514,9 @@ static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t se
     bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
     if (!g) return fail(BFSX_E_OOM, "graph");
     set_build_chunk(ctx->opt.build_chunk);
-    int rc = build_csr_kronecker(ctx->stream, scale, edgefactor, seed, ctx->opt.degree_order, &g->d_row_off,
-                                 &g->d_col, &g->nnz, &g->d_tuple_cnt, g->v_lo, g->nv);
+    int rc = build_csr_kronecker(ctx->stream, scale, edgefactor, seed, ctx->opt.degree_order,
+                                 ctx->opt.relabel && !dist, &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt,
+                                 &g->d_perm, &g->d_inv, g->v_lo, g->nv);
     (void)hipStreamSynchronize(ctx->stream);
     if (rc) {
         delete g;
@@ -494,12 +527,12 @@ static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t se
 }
 
 int bfsx_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, bfsx_graph **out) {
-    return graph_kronecker(ctx, scale, edgefactor, seed, 0, 1, out);
+    return graph_kronecker(ctx, scale, edgefactor, seed, 0, 1, out, false);
 }
 
 int bfsx_dist_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
                               bfsx_graph **out) {
-    return graph_kronecker(ctx, scale, edgefactor, seed, rank, nranks, out);
+    return graph_kronecker(ctx, scale, edgefactor, seed, rank, nranks, out, true);
 }
 
 int bfsx_graph_partition(const bfsx_graph *g, int64_t *nv_global, int64_t *v_lo, int64_t *nv_local, int64_t *chunk,
@@ -525,8 +558,10 @@ int bfsx_graph_degree(const bfsx_graph *g, int64_t v, int64_t *deg) {
     *deg = -1;
     if (v < g->v_lo || v >= g->v_lo + g->nv) return BFSX_OK;
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    int64_t x = 0;
+    if (int rc = to_internal(g, v, &x)) return rc;
     int64_t off[2];
-    BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + (v - g->v_lo), sizeof(off), hipMemcpyDeviceToHost));
+    BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + (x - g->v_lo), sizeof(off), hipMemcpyDeviceToHost));
     *deg = off[1] - off[0];
     return BFSX_OK;
 }
@@ -607,6 +642,8 @@ void bfsx_graph_free(bfsx_graph *g) {
     if (g->d_row_off) (void)hipFree(g->d_row_off);
     if (g->d_col) (void)hipFree(g->d_col);
     if (g->d_tuple_cnt) (void)hipFree(g->d_tuple_cnt);
+    if (g->d_perm) (void)hipFree(g->d_perm);
+    if (g->d_inv) (void)hipFree(g->d_inv);
     delete g;
 }
 
@@ -617,6 +654,8 @@ int64_t bfsx_graph_m(const bfsx_graph *g) { return g ? g->m : -1; }
 int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    if (g->d_perm) return export_csr_original(g->ctx->stream, g->nv, g->nnz, g->d_row_off, g->d_col, g->d_perm,
+                                              g->d_inv, row_off, col);
     if (row_off)
         BFSX_HIP_TRY(hipMemcpyAsync(row_off, g->d_row_off, (g->nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost,
                                     g->ctx->stream));
@@ -652,14 +691,16 @@ int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
         if (seen.count(x)) continue;
         int64_t ok = 0;
         if (x >= g->v_lo && x < g->v_lo + g->nv) {
+            int64_t xi = x; // internal id (relabelled single-device graphs)
+            if (int rc = to_internal(g, x, &xi)) return rc;
             int64_t off[2];
-            BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + (x - g->v_lo), sizeof(off), hipMemcpyDeviceToHost));
+            BFSX_HIP_TRY(hipMemcpy(off, g->d_row_off + (xi - g->v_lo), sizeof(off), hipMemcpyDeviceToHost));
             const int64_t deg = off[1] - off[0];
             ok = deg > 0;
             if (deg == 1) { // only neighbour may be a self-loop (Graph500: degree >= 1 excluding self-loops)
                 uint32_t nb = 0;
                 BFSX_HIP_TRY(hipMemcpy(&nb, g->d_col + off[0], sizeof(nb), hipMemcpyDeviceToHost));
-                ok = (int64_t)nb != x;
+                ok = (int64_t)nb != xi;
             }
         }
         if (part) {
@@ -681,9 +722,14 @@ int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_o
     if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: drive it with bfsx_dist_* (bfsx_dist.py)");
     const auto t0 = std::chrono::steady_clock::now();
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
+    if (source < 0 || source >= g->nv)
+        return fail(BFSX_E_RANGE, "source vertex " + std::to_string(source) + " outside [0, " + std::to_string(g->nv) +
+                                      ")");
+    int64_t si = source;
+    if (int rc = to_internal(g, source, &si)) return rc;
     bfsx_stats local{};
     const int64_t retries0 = bfs_persist_fallbacks(g);
-    int rc = bfs_run(g, source, &local);
+    int rc = bfs_run(g, si, &local);
     if (rc) return rc;
     local.persist_retries = (int32_t)(bfs_persist_fallbacks(g) - retries0);
     if (dist_out || parent_out) {
@@ -704,7 +750,13 @@ int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first
     if (!g) return fail(BFSX_E_ARG, "null graph");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     int64_t res[4] = {0, -1, 0, 0};
-    if (int rc = bfs_validate(g, source, nullptr, res)) return rc;
+    int64_t si = source;
+    if (source >= 0 && g->nranks == 1) {
+        if (source >= g->nv) return fail(BFSX_E_ARG, "source out of range");
+        if (int rc = to_internal(g, source, &si)) return rc;
+    }
+    if (int rc = bfs_validate(g, si, nullptr, res)) return rc;
+    if (int rc = to_original(g, res[1], &res[1])) return rc;
     if (errors) *errors = res[0];
     if (first_bad) *first_bad = res[1];
     if (reached) *reached = res[2];
@@ -717,16 +769,34 @@ int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, con
     if (!g || !dist || !parent) return fail(BFSX_E_ARG, "null argument");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     std::vector<unsigned long long> packed((size_t)g->nv);
-    for (int64_t i = 0; i < g->nv; i++)
-        packed[i] = ((unsigned long long)(uint32_t)parent[i] << 32) | (uint32_t)dist[i];
+    std::vector<uint32_t> perm;
+    int64_t si = source;
+    if (g->d_perm) { // the caller's arrays are indexed by original ids; the device checks internal ones
+        if (source < 0 || source >= g->nv) return fail(BFSX_E_ARG, "source out of range");
+        perm.resize((size_t)g->nv);
+        BFSX_HIP_TRY(hipMemcpy(perm.data(), g->d_perm, perm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        si = perm[(size_t)source];
+    }
+    for (int64_t i = 0; i < g->nv; i++) {
+        const int64_t p = parent[i];
+        uint32_t pw = (uint32_t)p;
+        if (!perm.empty() && p >= 0 && p < g->nv) pw = perm[(size_t)p];
+        const size_t at = perm.empty() ? (size_t)i : (size_t)perm[(size_t)i];
+        packed[at] = ((unsigned long long)pw << 32) | (uint32_t)dist[i];
+    }
     unsigned long long *d = nullptr;
     BFSX_HIP_TRY(hipMalloc(&d, std::max<size_t>(packed.size(), 1) * sizeof(unsigned long long)));
     hipError_t he = hipMemcpy(d, packed.data(), packed.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
     int64_t res[4] = {0, -1, 0, 0};
-    int rc = he == hipSuccess ? bfs_validate(g, source, d, res)
+    int rc = he == hipSuccess ? bfs_validate(g, si, d, res)
                               : fail(BFSX_E_HIP, std::string("validate upload: ") + hipGetErrorString(he));
     (void)hipFree(d);
     if (rc) return rc;
+    if (!perm.empty() && res[1] >= 0) {
+        uint32_t v = 0;
+        BFSX_HIP_TRY(hipMemcpy(&v, g->d_inv + res[1], sizeof(v), hipMemcpyDeviceToHost));
+        res[1] = v;
+    }
     if (errors) *errors = res[0];
     if (first_bad) *first_bad = res[1];
     return BFSX_OK;

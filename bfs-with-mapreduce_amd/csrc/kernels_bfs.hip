@@ -93,6 +93,9 @@ struct BfsWorkspace {
     int64_t hub_k = 0;                  // 0: off
     uint32_t *hub_id = nullptr;         // [hub_k] global id of hub h (degree descending)
     uint32_t hub_tdeg = 0xFFFFFFFFu;    // the hubs are exactly the vertices of degree >= hub_tdeg
+    // relabelled graph (ids in degree order): the hubs of the hybrid levels are the ids below hub_lim and
+    // need no encoded domain (their frontier bits are already the first hub_lim/64 words of the bitmap)
+    uint32_t hub_lim = 0;
     uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
     u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
@@ -302,6 +305,14 @@ __device__ inline bool claim(uint32_t v, u64 *vis, u64 &attempts) {
     return !(atomicOr(w, bit) & bit);
 }
 
+// The hub set of the hybrid levels (bfs_run): on a relabelled graph (ids in degree order) the ids below
+// `lim`, otherwise the vertices of degree >= `tdeg` (the encoded pull domain's members).  Off: {~0, 0}.
+struct HubSet {
+    uint32_t tdeg;
+    uint32_t lim;
+};
+__device__ inline bool is_hub(const HubSet &h, uint32_t v, u64 deg) { return v < h.lim || deg >= (u64)h.tdeg; }
+
 // 1-D partition of the vertex ids (multi-GPU path): this rank owns global ids [lo, lo+chunk) and
 // stores their rows; adjacency entries stay global.  Single-GPU graphs use lo = 0, one rank.
 struct Part {
@@ -352,7 +363,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
                                       int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
-                                      uint32_t t_hub, u64 &acc_mfh, u64 &acc_nh) {
+                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -387,7 +398,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
                 acc_mf += dg;
                 acc_dmax = dg > acc_dmax ? dg : acc_dmax;
-                if (dg >= t_hub) { // a hub of the bottom-up hub domain (hybrid levels, bfs_run)
+                if (is_hub(hs, v[k], dg)) { // a hub of the hybrid levels (bfs_run)
                     acc_mfh += dg;
                     acc_nh += 1;
                 }
@@ -406,8 +417,8 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
                                             LevelSlot *ring, int level, uint32_t hub_deg,
-                                            uint32_t *__restrict__ hubs, Part pt, int gsz, uint32_t t_hub,
-                                            uint32_t skip_deg) {
+                                            uint32_t *__restrict__ hubs, Part pt, int gsz, HubSet hs,
+                                            HubSet skip) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
@@ -437,7 +448,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                 // from (visited), so its row holds nothing to claim -- the frontier a pull level hands to
                 // a push level is mostly such leaves
                 d = 0;
-            } else if (d >= (int64_t)skip_deg) { // hybrid level: the bottom-up hub sweep covers this vertex
+            } else if (is_hub(skip, u + pt.lo, (u64)d)) { // hybrid level: the pull hub sweep covers this vertex
                 d = 0;
             } else if (d > (int64_t)hub_deg) {
                 hubs[atomicAdd(&cn->nhub, 1ull)] = u;
@@ -464,7 +475,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
         }
         __syncthreads();
         sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt, rq,
-                              acc_mf, attempts, acc_dmax, t_hub, acc_mfh, acc_nh);
+                              acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh);
         __syncthreads();
     }
     bq_flush(q, qout, &cn->qtail);
@@ -477,7 +488,7 @@ template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  u64 *vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
-                                                 Part pt, uint32_t t_hub) {
+                                                 Part pt, HubSet hs) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
@@ -534,7 +545,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
         sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt,
-                              rq, acc_mf, attempts, acc_dmax, t_hub, acc_mfh, acc_nh);
+                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh);
         __syncthreads();
     }
     bq_flush(q, qout, &cn->qtail);
@@ -631,7 +642,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
-                                                    PersistOut *out, uint32_t t_hub, int64_t bu_floor,
+                                                    PersistOut *out, HubSet hs, int64_t bu_floor,
                                                     int inject_abort) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
@@ -738,7 +749,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                         const u64 dg = (u64)(r1[k] - r0[k]);
                         acc_mf += dg;
                         acc_dmax = dg > acc_dmax ? dg : acc_dmax;
-                        acc_mfh += dg >= t_hub ? dg : 0ull;
+                        acc_mfh += is_hub(hs, v[k], dg) ? dg : 0ull;
                     }
                     const u64 mask = __ballot(win);
                     if (mask) {
@@ -1030,11 +1041,19 @@ __device__ inline uint32_t probe_bit(const u64 *__restrict__ front, const u64 *_
     return (w[(x >> 5) & 1u] >> (x & 31u)) & 1u;
 }
 
+// Whether adjacency entry x names a hub of the hybrid levels: the encoded domain's bit, or (relabelled
+// graph, plain ids) an id below the hub limit.
+template <bool kHubs>
+__device__ inline bool hub_entry(uint32_t x, uint32_t lim) {
+    return kHubs ? (x & kHubBit) != 0u : x < lim;
+}
+
 // Hub sweep (hybrid levels): only hub entries are probed; a non-hub entry reads as "not in frontier"
 // without a memory access (the frontier's non-hub vertices are expanded top-down in the same level).
 template <bool kHubs, bool kHubOnly>
-__device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *__restrict__ hfront, uint32_t x) {
-    if (kHubOnly && !(x & kHubBit)) return 0u;
+__device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *__restrict__ hfront, uint32_t x,
+                                     uint32_t lim) {
+    if (kHubOnly && !hub_entry<kHubs>(x, lim)) return 0u;
     return probe_bit<kHubs>(front, hfront, x);
 }
 
@@ -1048,7 +1067,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
-                                            const uint32_t *__restrict__ hub_id) {
+                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
@@ -1101,7 +1120,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                 uint32_t fbm = 0u; // bit k: candidate k's top1 is in the frontier
 #pragma unroll
                 for (int k = 0; k < kU; k++)
-                    fbm |= ((t0 + (uint32_t)k * 64 + lane < he) && (!kHubOnly || (x[k] & kHubBit))
+                    fbm |= ((t0 + (uint32_t)k * 64 + lane < he) && (!kHubOnly || hub_entry<kHubs>(x[k] & ~fmask, hub_lim))
                                 ? probe_bit<kHubs>(front, hfront, x[k] & ~fmask)
                                 : 0u)
                            << k;
@@ -1110,7 +1129,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
                     const bool a2 = (t0 + (uint32_t)k * 64 + lane < he) && !((fbm >> k) & 1u) && !(x[k] & fmask) &&
-                                    (!kHubOnly || (x[k] & kHubBit));
+                                    (!kHubOnly || hub_entry<kHubs>(x[k] & ~fmask, hub_lim));
                     r[k] = a2 ? rest[v[k]] : make_uint4(0u, 0u, 0u, 0u);
                     acc_s2 += a2;
                 }
@@ -1118,9 +1137,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
                     if (r[k].w != 0u) {
-                        pbm |= (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].x) |
-                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].y) << 1) |
-                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].z) << 2))
+                        pbm |= (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].x, hub_lim) |
+                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].y, hub_lim) << 1) |
+                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].z, hub_lim) << 2))
                                << (3 * k);
                     }
                 }
@@ -1141,14 +1160,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                         } else if (deg1) {
                             acc_mu += 1;
                             acc_sc += 1;
-                        } else if (kHubOnly && !(x[k] & kHubBit)) {
+                        } else if (kHubOnly && !hub_entry<kHubs>(x[k] & ~fmask, hub_lim)) {
                             acc_mu += 1; // no hub in the row (degree unknown here; the next pull level recounts m_u)
                             acc_sc += 1;
                         } else if (pb) {
                             found = true;
                             par = (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z;
                             acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
-                        } else if (deg <= 4u || (kHubOnly && !(r[k].x & r[k].y & r[k].z & kHubBit))) {
+                        } else if (deg <= 4u || (kHubOnly && !(hub_entry<kHubs>(r[k].x, hub_lim) &&
+                                                               hub_entry<kHubs>(r[k].y, hub_lim) &&
+                                                               hub_entry<kHubs>(r[k].z, hub_lim)))) {
                             acc_mu += deg; // row exhausted (or, hub sweep: its hub prefix is)
                             acc_sc += deg < 4u ? deg : 4u;
                         } else {
@@ -1181,10 +1202,10 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                             const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                             const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                             const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                            const uint32_t h0 = probe_hub<kHubs, kHubOnly>(front, hfront, x0);
-                            const uint32_t h1 = probe_hub<kHubs, kHubOnly>(front, hfront, x1);
-                            const uint32_t h2 = probe_hub<kHubs, kHubOnly>(front, hfront, x2);
-                            const uint32_t h3 = probe_hub<kHubs, kHubOnly>(front, hfront, x3);
+                            const uint32_t h0 = probe_hub<kHubs, kHubOnly>(front, hfront, x0, hub_lim);
+                            const uint32_t h1 = probe_hub<kHubs, kHubOnly>(front, hfront, x1, hub_lim);
+                            const uint32_t h2 = probe_hub<kHubs, kHubOnly>(front, hfront, x2, hub_lim);
+                            const uint32_t h3 = probe_hub<kHubs, kHubOnly>(front, hfront, x3, hub_lim);
                             if (h0 | h1 | h2 | h3) {
                                 found = true;
                                 const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
@@ -1194,7 +1215,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                                 j += left < 4 ? left : 4;
                                 // hub sweep: rows are degree-ordered, so past the first non-hub entry no
                                 // hub follows
-                                if (kHubOnly) stop = !(x0 & x1 & x2 & x3 & kHubBit);
+                                if (kHubOnly)
+                                    stop = !(hub_entry<kHubs>(x0, hub_lim) && hub_entry<kHubs>(x1, hub_lim) &&
+                                             hub_entry<kHubs>(x2, hub_lim) && hub_entry<kHubs>(x3, hub_lim));
                             }
                         }
                         acc_sc += (uint32_t)(j - b - 4);
@@ -1323,6 +1346,18 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, int
         const u64 s = stt[i];
         dist[i] = (int32_t)(uint32_t)s;
         parent[i] = (int32_t)(uint32_t)(s >> 32);
+    }
+}
+
+// The same for a relabelled graph: internal row i is original vertex inv[i]; parents map back too.
+__global__ __launch_bounds__(kBS) void k_unpack_relabel(const u64 *__restrict__ stt, const uint32_t *__restrict__ inv,
+                                                        int64_t n, int32_t *__restrict__ dist,
+                                                        int32_t *__restrict__ parent) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        const u64 s = stt[i];
+        const uint32_t o = inv[i], p = (uint32_t)(s >> 32);
+        dist[o] = (int32_t)(uint32_t)s;
+        parent[o] = p == 0xFFFFFFFFu ? -1 : (int32_t)inv[p];
     }
 }
 
@@ -1498,7 +1533,19 @@ unsigned clamp_grid(int64_t blocks, unsigned cap) {
 int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     const int hb = g->ctx->opt.hub_bits;
     const bool part = g->nranks > 1;
-    if (hb == 0 || g->nv_global > ((int64_t)1 << 30) || g->nv_global < 64) return BFSX_OK;
+    if (hb == 0 || g->nv_global < 64) return BFSX_OK;
+    if (g->d_perm) { // relabelled: hubs = the first k ids (the k highest degrees), nothing to build
+        int64_t k = 64;
+        if (hb < 0) {
+            if (g->nv < ((int64_t)1 << 16)) return BFSX_OK;
+            while (k * 1024 < g->nv) k *= 2;
+        } else {
+            k = (int64_t)1 << hb;
+        }
+        ws->hub_lim = (uint32_t)std::min<int64_t>(k, g->nv);
+        return BFSX_OK;
+    }
+    if (g->nv_global > ((int64_t)1 << 30)) return BFSX_OK;
     Comm *cm = g->ctx->comm.get();
     // a partition ranks the hubs by GLOBAL degree: the degrees are all-gathered over the communicator
     // (collective -- every rank reaches this at its first BFS); a partition driven without one (the
@@ -1665,6 +1712,11 @@ int ws_alloc(bfsx_graph *g) {
 }
 
 // ---- launch helpers: one per traversal kernel, dispatching on the row-offset width -------------
+HubSet hub_set(const BfsWorkspace *ws) {
+    return HubSet{ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, ws->hub_lim};
+}
+bool has_hubs(const BfsWorkspace *ws) { return ws->hub_k > 0 || ws->hub_lim > 0; }
+
 // dmax: largest degree in the frontier (< 0: unknown) -- the hub bin is skipped when no vertex exceeds
 // the hub degree
 // skip_hubs (hybrid level): frontier vertices of the hub domain are left to the bottom-up hub sweep.
@@ -1672,8 +1724,8 @@ template <bool kDist>
 int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt,
               bool skip_hubs = false) {
     hipStream_t st = g->ctx->stream;
-    const uint32_t t_hub = ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu;
-    const uint32_t skip_deg = skip_hubs ? t_hub : 0xFFFFFFFFu;
+    const HubSet hs = hub_set(ws);
+    const HubSet skip = skip_hubs ? hs : HubSet{0xFFFFFFFFu, 0u};
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     const uint32_t hub_deg = g->ctx->opt.hub_degree;
     int gsz = 16;
@@ -1684,20 +1736,20 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, t_hub, skip_deg);
+                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, t_hub);
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs);
             BFSX_HIP_TRY(hipGetLastError());
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, t_hub, skip_deg);
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, t_hub);
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs);
             BFSX_HIP_TRY(hipGetLastError());
         }
     }
@@ -1724,8 +1776,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     }
     hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
                        ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
-                       ws->top1_flag,
-                       ws->hfront, ws->hub_id);
+                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -1738,8 +1789,11 @@ int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
 
 // The bottom-up half of a hybrid level: candidates probe only the hubs of the frontier (single device).
 int launch_bu_hubonly(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
-    return ws->off32 ? launch_bu_u<uint32_t, false, true, 4, true>(g, ws, ws->off32, front, level)
-                     : launch_bu_u<int64_t, false, true, 4, true>(g, ws, g->d_row_off, front, level);
+    if (ws->hub_k > 0)
+        return ws->off32 ? launch_bu_u<uint32_t, false, true, 4, true>(g, ws, ws->off32, front, level)
+                         : launch_bu_u<int64_t, false, true, 4, true>(g, ws, g->d_row_off, front, level);
+    return ws->off32 ? launch_bu_u<uint32_t, false, false, 4, true>(g, ws, ws->off32, front, level)
+                     : launch_bu_u<int64_t, false, false, 4, true>(g, ws, g->d_row_off, front, level);
 }
 
 template <bool kMf>
@@ -1892,12 +1946,12 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws), opt.persist_abort_at);
+                           hub_set(ws), bu_floor(ws), opt.persist_abort_at);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           ws->hub_k > 0 ? ws->hub_tdeg : 0xFFFFFFFFu, bu_floor(ws), opt.persist_abort_at);
+                           hub_set(ws), bu_floor(ws), opt.persist_abort_at);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -1993,7 +2047,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t mu = g->nnz;                  // Beamer m_u: adjacency entries of unvisited vertices
     // degree sum of the frontier's hub-domain vertices (-1: unknown): a top-down level whose frontier
     // degree sum sits mostly in hubs runs as a hybrid level (below)
-    int64_t mfh = (ws->hub_k > 0 && mf >= (int64_t)ws->hub_tdeg) ? mf : 0;
+    int64_t mfh = ((ws->hub_k > 0 && mf >= (int64_t)ws->hub_tdeg) || source < (int64_t)ws->hub_lim) ? mf : 0;
     int64_t examined = 0, visited = 1;
     int td_levels = 0, bu_levels = 0;
     std::vector<LevelTiming> timing;
@@ -2027,7 +2081,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         // walk their whole hub prefix), the push level ~0.028 ms per million frontier edges (0.72 ms at
         // 17.6 M, 1.74 ms at 67.4 M) -- so hybrid only once the hubs' edges exceed 1.25 U.
         bool hybrid = false;
-        if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && ws->hub_k > 0 && opt.hybrid != 0 && mfh > 0) {
+        if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && has_hubs(ws) && opt.hybrid != 0 && mfh > 0) {
             const int64_t unv = nv - visited - ws->n_dead;
             hybrid = opt.hybrid == 2 || 4 * mfh > 5 * unv;
         }
@@ -2128,7 +2182,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                     nf = ls.frontier_out;
                     mf = (int64_t)r.mf;
                     dmax = (int64_t)r.dmax;
-                    mfh = ws->hub_k > 0 ? (int64_t)r.mfh : -1;
+                    mfh = has_hubs(ws) ? (int64_t)r.mfh : -1;
                 }
                 std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
                 td_levels += ran;
@@ -2186,7 +2240,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             mu -= s.mf;
             mf = s.mf;
             dmax = ws->h_pub->dmax;
-            mfh = ws->hub_k > 0 ? s.s2 : -1; // top-down: stage2 = degree sum of the hubs discovered
+            mfh = has_hubs(ws) ? s.s2 : -1; // top-down: stage2 = degree sum of the hubs discovered
             std::swap(ws->qa, ws->qb);
         } else {
             mu = s.mu; // exact: degree sum of the candidates this level left unvisited
@@ -2260,8 +2314,12 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     const size_t nv = (size_t)g->nv;
     // unpack into the (idle) frontier queues, then D2H
     int32_t *d_dist = reinterpret_cast<int32_t *>(ws->qa), *d_par = reinterpret_cast<int32_t *>(ws->qb);
-    hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
-                       (int64_t)nv, d_dist, d_par);
+    if (g->d_inv)
+        hipLaunchKernelGGL(k_unpack_relabel, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                           ws->st, g->d_inv, (int64_t)nv, d_dist, d_par);
+    else
+        hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
+                           (int64_t)nv, d_dist, d_par);
     BFSX_HIP_TRY(hipGetLastError());
     if (dist_out) BFSX_HIP_TRY(hipMemcpyAsync(dist_out, d_dist, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (parent_out) {

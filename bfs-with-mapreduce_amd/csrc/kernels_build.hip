@@ -14,6 +14,7 @@
 // built straight from the counter stream (every pass regenerates its tuples, none are stored).
 #include <cstring>
 
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
@@ -121,6 +122,19 @@ struct ArraySrc {
 struct KronSrc {
     KronParams p;
     __device__ void operator()(int64_t i, uint32_t &a, uint32_t &b) const { kron_tuple(p, i, a, b); }
+};
+
+// The same tuples with both endpoints renamed through `perm` (the degree-descending relabel below).
+template <class Src>
+struct PermSrc {
+    Src s;
+    const uint32_t *perm;
+    __device__ void operator()(int64_t i, uint32_t &a, uint32_t &b) const {
+        uint32_t x, y;
+        s(i, x, y);
+        a = perm[x];
+        b = perm[y];
+    }
 };
 
 
@@ -319,8 +333,8 @@ int order_rows_by_degree(hipStream_t stream, const int64_t *d_off, int64_t nv, i
 namespace {
 
 template <class Src>
-int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_order, int64_t **d_row_off_out,
-                   uint32_t **d_col_out, int64_t *nnz_out, uint32_t **d_tuple_cnt_out, int64_t lo, int64_t nv_global) {
+int build_rows(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_order, int64_t **d_row_off_out,
+               uint32_t **d_col_out, int64_t *nnz_out, uint32_t **d_tuple_cnt_out, int64_t lo, int64_t nv_global) {
     if (nv_global < 0) nv_global = nv;
     const bool partitioned = lo != 0 || nv != nv_global;
     DevBuf<uint32_t> deg, tcnt;
@@ -453,21 +467,165 @@ int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degr
     return BFSX_OK;
 }
 
-} // namespace
-
-int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
-                     bool degree_order, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt,
-                     int64_t lo, int64_t nv_global) {
-    return build_csr_impl(stream, nv, ArraySrc{d_u, d_v}, m, degree_order, d_row_off, d_col, nnz, d_tuple_cnt, lo,
-                          nv_global);
+// Degree-descending relabel keys: ~degree (so an ascending sort puts the highest degree first), ids.
+__global__ __launch_bounds__(kBS) void k_rank_keys(const uint32_t *__restrict__ deg, int64_t n,
+                                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < n; v += (int64_t)gridDim.x * kBS) {
+        keys[v] = ~deg[v];
+        ids[v] = (uint32_t)v;
+    }
 }
 
-int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order,
-                        int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, int64_t lo,
-                        int64_t nv_local) {
+__global__ __launch_bounds__(kBS) void k_invert(const uint32_t *__restrict__ inv, int64_t n, uint32_t *__restrict__ perm) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS)
+        perm[inv[i]] = (uint32_t)i;
+}
+
+// Single-device graphs (lo = 0, nv = nv_global) with relabel: the vertices are renumbered by degree,
+// descending (tuple-endpoint degree: duplicates counted, a self-loop once; ties by id), and the CSR is
+// built from the renamed tuples.  Internal id order is then degree order, so
+//   - rows sorted ascending by internal id ARE degree-ordered (no second sort of the adjacency);
+//   - the high-degree vertices every pull probe and push claim concentrates on occupy the first
+//     lines of the frontier / visited bitmaps, the state array and top1/rest (cache-resident), and
+//     the "hubs" of the hybrid levels are simply the ids below a limit;
+//   - isolated vertices sit at the end, in whole words the pull kernel skips with one branch.
+// perm[original] = internal, inv[internal] = original; the C-ABI maps sources and results through them.
+template <class Src>
+int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_order, bool relabel,
+                   int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out, uint32_t **d_tuple_cnt_out,
+                   uint32_t **d_perm_out, uint32_t **d_inv_out, int64_t lo, int64_t nv_global) {
+    if (nv_global < 0) nv_global = nv;
+    if (!relabel || lo != 0 || nv != nv_global || !degree_order)
+        return build_rows(stream, nv, src, m, degree_order, d_row_off_out, d_col_out, nnz_out, d_tuple_cnt_out, lo,
+                          nv_global);
+    DevBuf<uint32_t> perm, inv;
+    {
+        DevBuf<uint32_t> deg, tcnt, keys, keys2, ids;
+        BFSX_HIP_TRY(deg.alloc(nv + 1));
+        BFSX_HIP_TRY(tcnt.alloc(nv));
+        BFSX_HIP_TRY(hipMemsetAsync(deg.p, 0, (nv + 1) * sizeof(uint32_t), stream));
+        BFSX_HIP_TRY(hipMemsetAsync(tcnt.p, 0, nv * sizeof(uint32_t), stream));
+        if (m > 0) {
+            hipLaunchKernelGGL(k_count<Src>, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, src, m, 0u, (uint32_t)nv,
+                               deg.p, tcnt.p);
+            BFSX_HIP_TRY(hipGetLastError());
+        }
+        tcnt.reset();
+        BFSX_HIP_TRY(keys.alloc(nv));
+        BFSX_HIP_TRY(keys2.alloc(nv));
+        BFSX_HIP_TRY(ids.alloc(nv));
+        BFSX_HIP_TRY(inv.alloc(nv));
+        hipLaunchKernelGGL(k_rank_keys, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, deg.p, nv, keys.p, ids.p);
+        BFSX_HIP_TRY(hipGetLastError());
+        size_t tb = 0;
+        BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys.p, keys2.p, ids.p, inv.p, (size_t)nv, 0, 32, stream));
+        DevBuf<char> tmp;
+        BFSX_HIP_TRY(tmp.alloc(tb));
+        BFSX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tb, keys.p, keys2.p, ids.p, inv.p, (size_t)nv, 0, 32, stream));
+        BFSX_HIP_TRY(perm.alloc(nv));
+        hipLaunchKernelGGL(k_invert, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, inv.p, nv, perm.p);
+        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_HIP_TRY(hipStreamSynchronize(stream)); // temporaries are freed at the end of this scope
+    }
+    // ascending rows of internal ids are degree-descending rows: no degree-order pass
+    int rc = build_rows(stream, nv, PermSrc<Src>{src, perm.p}, m, false, d_row_off_out, d_col_out, nnz_out,
+                        d_tuple_cnt_out, 0, nv_global);
+    if (rc) return rc;
+    *d_perm_out = perm.release();
+    *d_inv_out = inv.release();
+    return BFSX_OK;
+}
+
+} // namespace
+
+namespace {
+
+__global__ __launch_bounds__(kBS) void k_orig_deg(const uint32_t *__restrict__ perm, const int64_t *__restrict__ off,
+                                                  int64_t nv, int64_t *__restrict__ deg) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
+        const uint32_t x = perm[v];
+        deg[v] = off[x + 1] - off[x];
+    }
+}
+
+// Original rows [r0, r1): one wave per row, entries mapped back to original ids, written at
+// off_o[v] - e0 of the chunk buffer.
+__global__ __launch_bounds__(kBS) void k_orig_rows(const uint32_t *__restrict__ perm, const uint32_t *__restrict__ inv,
+                                                   const int64_t *__restrict__ off, const uint32_t *__restrict__ col,
+                                                   const int64_t *__restrict__ off_o, int64_t r0, int64_t r1, int64_t e0,
+                                                   uint32_t *__restrict__ out) {
+    const unsigned lane = threadIdx.x & 63u;
+    const int64_t nw = ((int64_t)gridDim.x * kBS) >> 6;
+    for (int64_t v = r0 + (((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6); v < r1; v += nw) {
+        const uint32_t x = perm[v];
+        const int64_t b = off[x], e = off[x + 1], o = off_o[v] - e0;
+        for (int64_t j = b + lane; j < e; j += 64) out[o + (j - b)] = inv[col[j]];
+    }
+}
+
+} // namespace
+
+int export_csr_original(hipStream_t stream, int64_t nv, int64_t nnz, const int64_t *d_row_off, const uint32_t *d_col,
+                        const uint32_t *d_perm, const uint32_t *d_inv, int64_t *row_off, uint32_t *col) {
+    DevBuf<int64_t> deg, off_o;
+    BFSX_HIP_TRY(deg.alloc(nv + 1));
+    BFSX_HIP_TRY(off_o.alloc(nv + 1));
+    BFSX_HIP_TRY(hipMemsetAsync(deg.p + nv, 0, sizeof(int64_t), stream));
+    hipLaunchKernelGGL(k_orig_deg, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, d_perm, d_row_off, nv, deg.p);
+    BFSX_HIP_TRY(hipGetLastError());
+    {
+        size_t tb = 0;
+        BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, tb, deg.p, off_o.p, (int64_t)0, (size_t)(nv + 1),
+                                             rocprim::plus<int64_t>(), stream));
+        DevBuf<char> tmp;
+        BFSX_HIP_TRY(tmp.alloc(tb));
+        BFSX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tb, deg.p, off_o.p, (int64_t)0, (size_t)(nv + 1),
+                                             rocprim::plus<int64_t>(), stream));
+        BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    }
+    std::vector<int64_t> h_own;
+    int64_t *h_off = row_off;
+    if (!h_off) {
+        h_own.resize(nv + 1);
+        h_off = h_own.data();
+    }
+    BFSX_HIP_TRY(hipMemcpy(h_off, off_o.p, (nv + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (!col || nnz <= 0) return BFSX_OK;
+    // rows in chunks of <= 2^28 entries (one temporary of 1 GiB at most, whatever the graph's size)
+    std::vector<int64_t> h_vec;
+    if (!h_own.empty()) h_vec.swap(h_own);
+    const std::vector<int64_t> &hv = h_vec.empty() ? std::vector<int64_t>(h_off, h_off + nv + 1) : h_vec;
+    std::vector<int64_t> cuts;
+    if (int rc = plan_row_chunks(hv, nv, (int64_t)1 << 28, cuts)) return rc;
+    int64_t cap = 0;
+    for (size_t c = 0; c + 1 < cuts.size(); c++) cap = std::max(cap, hv[cuts[c + 1]] - hv[cuts[c]]);
+    DevBuf<uint32_t> buf;
+    BFSX_HIP_TRY(buf.alloc(cap));
+    for (size_t c = 0; c + 1 < cuts.size(); c++) {
+        const int64_t r0 = cuts[c], r1 = cuts[c + 1], e0 = hv[r0], n = hv[r1] - e0;
+        if (n <= 0) continue;
+        hipLaunchKernelGGL(k_orig_rows, dim3(grid_for((r1 - r0) * 64, kBS)), dim3(kBS), 0, stream, d_perm, d_inv,
+                           d_row_off, d_col, off_o.p, r0, r1, e0, buf.p);
+        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_HIP_TRY(hipMemcpyAsync(col + e0, buf.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        BFSX_HIP_TRY(hipStreamSynchronize(stream));
+    }
+    return BFSX_OK;
+}
+
+int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
+                     bool degree_order, bool relabel, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
+                     uint32_t **d_tuple_cnt, uint32_t **d_perm, uint32_t **d_inv, int64_t lo, int64_t nv_global) {
+    return build_csr_impl(stream, nv, ArraySrc{d_u, d_v}, m, degree_order, relabel, d_row_off, d_col, nnz,
+                          d_tuple_cnt, d_perm, d_inv, lo, nv_global);
+}
+
+int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order, bool relabel,
+                        int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, uint32_t **d_perm,
+                        uint32_t **d_inv, int64_t lo, int64_t nv_local) {
     const int64_t m = (int64_t)edgefactor << scale;
-    return build_csr_impl(stream, nv_local, KronSrc{kron_params(scale, seed)}, m, degree_order, d_row_off, d_col,
-                          nnz, d_tuple_cnt, lo, (int64_t)1 << scale);
+    return build_csr_impl(stream, nv_local, KronSrc{kron_params(scale, seed)}, m, degree_order, relabel, d_row_off,
+                          d_col, nnz, d_tuple_cnt, d_perm, d_inv, lo, (int64_t)1 << scale);
 }
 
 } // namespace bfsx

@@ -165,14 +165,19 @@ def test_kronecker_bfs_parity(ctx, scale):
         assert len(dirs) > 0
 
 
+@pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("order", ["id", "degree"])
-def test_row_order_option(ctx, order):
-    """Rows in id order are sorted ascending; both orders give identical distances."""
+def test_row_order_option(ctx, order, relabel):
+    """Rows in id order are sorted ascending; both orders give identical distances.  Degree order:
+    relabel off sorts each row by neighbour degree (after dedup); relabel on (the default) renumbers the
+    vertices by tuple-endpoint degree (duplicates counted, ties by id), so a row ascending in internal
+    ids is that order -- the exported CSR (original ids) shows it row by row."""
     seed, scale = 77, 12
     ou, ov = O.kronecker(scale, 16, seed)
     nv = 1 << scale
     off, col = O.build_sets(nv, ou, ov)
     ctx.set_option("row_order", order)
+    ctx.set_option("relabel", relabel)
     try:
         with ctx.kronecker(scale, 16, seed) as g:
             goff, gcol = g.csr()
@@ -180,13 +185,22 @@ def test_row_order_option(ctx, order):
                 assert np.array_equal(gcol, col)
             else:
                 assert same_sets(off, col, goff, gcol)
-                deg = np.diff(off)
-                for x in range(0, nv, 97):  # non-increasing neighbour degree inside a row
-                    assert np.all(np.diff(deg[gcol[goff[x]:goff[x + 1]]]) <= 0)
+                if relabel == "off":
+                    key = np.diff(off).astype(np.int64) * nv  # dedup degree; ties in any order
+                    tie = np.zeros(nv, np.int64)
+                else:
+                    raw = np.bincount(ou, minlength=nv) + np.bincount(ov[ov != ou], minlength=nv)
+                    key = raw.astype(np.int64) * nv
+                    tie = np.arange(nv, dtype=np.int64)  # equal raw degree: ascending id
+                for x in range(0, nv, 97):  # non-increasing (degree, -id) inside a row
+                    r = gcol[goff[x]:goff[x + 1]]
+                    assert np.all(np.diff(key[r] - tie[r]) <= 0) if relabel == "on" else \
+                        np.all(np.diff(key[r]) <= 0)
             r = int(g.sample_roots(1, seed=9)[0])
             check_against_oracle(g, nv, off, col, r, ou, ov)
     finally:
         ctx.set_option("row_order", "degree")
+        ctx.set_option("relabel", "on")
 
 
 @pytest.mark.parametrize("blocks", ["auto", "3"])
@@ -358,15 +372,17 @@ def test_repeated_bfs_reuses_state(ctx):
         assert np.array_equal(d2, d0)
 
 
+@pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("bits", ["off", "1", "6", "12", "30"])
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
-def test_hub_probe_domain(ctx, bits, direction):
-    """k_bu's hub-encoded probes (option hub_bits: 2^b highest-degree vertices get a dense second id;
-    30 = every vertex is a hub, 1 = two hubs): distances bit-exact and parents valid whatever the hub
-    count, on edge-case graphs and a scale-14 Kronecker graph."""
+def test_hub_probe_domain(ctx, bits, direction, relabel):
+    """Hub sets of every size (option hub_bits: the 2^b highest-degree vertices; 30 = every vertex is a
+    hub, 1 = two hubs): relabel off = k_bu's hub-encoded probe domain (a dense second id per hub); relabel
+    on = ids below a limit.  Distances bit-exact and parents valid on edge-case graphs and scale 14."""
     cases = [c for c in random_cases() if c[0] in ("rand3", "star", "multi_hub", "two_comp", "isolated", "dups")]
     ctx.set_option("hub_bits", bits)
     ctx.set_option("direction", direction)
+    ctx.set_option("relabel", relabel)
     try:
         for name, nv, u, v in cases:
             u = np.asarray(u, np.uint32)
@@ -384,15 +400,25 @@ def test_hub_probe_domain(ctx, bits, direction):
     finally:
         ctx.set_option("hub_bits", "auto")
         ctx.set_option("direction", "auto")
+        ctx.set_option("relabel", "on")
 
 
+def raw_degree(nv, u, v):
+    """Tuple-endpoint degree (duplicates counted, a self-loop once): the relabel's sort key."""
+    u = np.asarray(u, np.int64)
+    v = np.asarray(v, np.int64)
+    return np.bincount(u, minlength=nv) + np.bincount(v[v != u], minlength=nv)
+
+
+@pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("chunk", ["1", "37", "5000"])
-def test_chunked_csr_build(ctx, chunk):
+def test_chunked_csr_build(ctx, chunk, relabel):
     """The CSR build sorts/dedups/orders rows in chunks of `build_chunk` raw entries, compacting in place
     (what lets scale 30 build on one device).  Tiny chunks (1 = one row per chunk, rows longer than the
     chunk, chunk edges inside duplicate runs) must give the same neighbour sets and degree order."""
     cases = [c for c in random_cases() if c[0] in ("rand0", "rand5", "star", "dups", "self_loops", "isolated")]
     ctx.set_option("build_chunk", chunk)
+    ctx.set_option("relabel", relabel)
     try:
         for name, nv, u, v in cases:
             u = np.asarray(u, np.uint32)
@@ -401,9 +427,10 @@ def test_chunked_csr_build(ctx, chunk):
             with ctx.from_edges(nv, u, v) as g:
                 goff, gcol = g.csr()
                 assert same_sets(off, col, goff, gcol), name
-                # degree-descending order inside every row (ties by id)
-                deg = np.diff(goff)
-                rows = np.repeat(np.arange(nv), deg)
+                # degree-descending order inside every row (ties by id): the dedup degree, or with the
+                # relabel the tuple-endpoint degree it sorts by
+                deg = np.diff(goff) if relabel == "off" else raw_degree(nv, u, v)
+                rows = np.repeat(np.arange(nv), np.diff(goff))
                 key = np.lexsort((gcol, -deg[gcol], rows))
                 assert np.array_equal(gcol[key], gcol), name
                 check_against_oracle(g, nv, off, col, 0, u, v, mr=False)
@@ -414,6 +441,7 @@ def test_chunked_csr_build(ctx, chunk):
             assert same_sets(off, col, goff, gcol)
     finally:
         ctx.set_option("build_chunk", str(1 << 30))
+        ctx.set_option("relabel", "on")
 
 
 @pytest.mark.parametrize("unroll", ["2", "4"])
@@ -442,13 +470,15 @@ def test_bottomup_unroll_variants(ctx, unroll):
             ctx.set_option(k, val)
 
 
+@pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("bits", ["2", "6", "30"])
-def test_hybrid_levels(ctx, bits):
+def test_hybrid_levels(ctx, bits, relabel):
     """Hybrid levels (pull from the frontier's hubs + push from its other vertices; option hybrid=force
     runs every top-down level whose frontier holds a hub that way): bit-exact distances, valid parents
     and the same pass count, whatever the hub count (30 = every vertex is a hub: the push half is empty;
     2 = four hubs: most of the frontier is pushed)."""
     ctx.set_option("hub_bits", bits)
+    ctx.set_option("relabel", relabel)
     ctx.set_option("hybrid", "force")
     ctx.set_option("persist", "off")  # every level through the per-level loop (persist=on is covered below)
     try:
@@ -476,6 +506,7 @@ def test_hybrid_levels(ctx, bits):
         ctx.set_option("hub_bits", "auto")
         ctx.set_option("hybrid", "auto")
         ctx.set_option("persist", "on")
+        ctx.set_option("relabel", "on")
 
 
 @pytest.mark.parametrize("direction", ["topdown", "auto", "bottomup"])
