@@ -310,6 +310,13 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.persist_abort_at = (int)x;
         return BFSX_OK;
     }
+    if (k == "persist_dmax") {
+        char *end = nullptr;
+        const long long x = strtoll(value, &end, 10);
+        if (!end || *end || x < 1) return fail(BFSX_E_ARG, "persist_dmax must be a degree >= 1");
+        ctx->opt.persist_dmax = x;
+        return BFSX_OK;
+    }
     if (k == "slot_pairs") {
         char *end = nullptr;
         const long long x = strtoll(value, &end, 10);
@@ -328,6 +335,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         if (v == "2") ctx->opt.bu_unroll = 2;
         else if (v == "4") ctx->opt.bu_unroll = 4;
         else return fail(BFSX_E_ARG, "bu_unroll must be 2|4");
+        return BFSX_OK;
+    }
+    if (k == "bu_pipeline") {
+        if (v == "on") ctx->opt.bu_pipeline = true;
+        else if (v == "off") ctx->opt.bu_pipeline = false;
+        else return fail(BFSX_E_ARG, "bu_pipeline must be on|off");
         return BFSX_OK;
     }
     if (k == "build_chunk") {

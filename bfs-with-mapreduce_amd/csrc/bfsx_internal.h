@@ -36,10 +36,12 @@ struct Options {
     bool relabel = true;        // single-device graphs: vertices renumbered by degree (desc) at build
     int hub_bits = -1;          // bottom-up hub probe domain: -1 auto, 0 off, b = 2^b hubs
     int bu_unroll = 4;          // bottom-up candidates per lane per round (4 or 2)
+    bool bu_pipeline = true;    // bottom-up: the next round's top1 loads overlap this round (kU = 4)
     int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
     int persist_abort_at = -1;  // test hook: K3p aborts at this level of its launch (-1: never)
+    int64_t persist_dmax = 2048; // K3p only while every frontier vertex has at most this degree
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------

@@ -53,11 +53,19 @@ constexpr int kStatFields = 7; // summed fields, in declaration order (dmax is a
 
 // Counters of one level.  Level L reads slot L%3 (its own frontier, already on the host), accumulates
 // the frontier it produces into slot (L+1)%3 and zeroes slot (L+2)%3: no per-level memset.
+struct alignas(64) DoneShard {
+    u64 n;
+    u64 pad[7];
+};
+constexpr int kDoneShards = 8; // arrival counters of publish_if_last, one line each (blockIdx % 8)
+
 struct LevelSlot {
     u64 qtail; // top-down next-queue allocation cursor (= frontier size produced)
     u64 nhub;  // top-down hub-list length
-    u64 pad[6];
+    u64 done;  // shards of the publishing kernel whose workgroups have all finished (publish_if_last)
+    u64 pad[5];
     StatShard sh[kShards];
+    DoneShard dsh[kDoneShards]; // finished workgroups of the publishing kernel, per blockIdx % 8
 };
 constexpr int kSlotWords = (int)(sizeof(LevelSlot) / sizeof(u64));
 
@@ -70,7 +78,7 @@ struct alignas(64) PersistRec {
 };
 constexpr int kRecWords = 5; // per-workgroup record words of a K3p level
 
-// A level's counter sums as the host reads them (mapped pinned memory, written by k_publish).
+// A level's counter sums as the host reads them (mapped pinned memory, written by publish_if_last).
 struct alignas(64) Published {
     u64 seq;
     int64_t qtail, nf, mf, sc, cl, mu, dmax, stage2, walked;
@@ -220,26 +228,61 @@ __global__ __launch_bounds__(kBS) void k_init(uint32_t s, uint32_t sglob, int64_
     zero_slot(ring, -1); // slot 1
 }
 
-// ---- level counters -> host: sums of the level's stat shards, published into mapped pinned host
+// ---- level counters -> host: the sums of the level's stat shards are published into mapped pinned host
 // memory with a sequence number the host spins on (a D2H copy + stream synchronise costs ~15 us per
-// level on MI355X, this ~9 us) ------------------------------------------------------------------
-__global__ void k_publish(const LevelSlot *__restrict__ slot, Published *pub, u64 seq) {
-    const unsigned lane = threadIdx.x; // one wave, lane i sums shard i
-    const StatShard &sh = slot->sh[lane];
-    const u64 nf = wave_sum(sh.nf), mf = wave_sum(sh.mf), sc = wave_sum(sh.scanned), cl = wave_sum(sh.claims),
-              mu = wave_sum(sh.mu), dmax = wave_max(sh.dmax), s2 = wave_sum(sh.stage2), wk = wave_sum(sh.walked);
-    if (lane == 0) {
-        pub->stage2 = (int64_t)s2;
-        pub->walked = (int64_t)wk;
-        pub->qtail = (int64_t)slot->qtail;
-        pub->nf = (int64_t)nf;
-        pub->mf = (int64_t)mf;
-        pub->sc = (int64_t)sc;
-        pub->cl = (int64_t)cl;
-        pub->mu = (int64_t)mu;
-        pub->dmax = (int64_t)dmax;
-        __threadfence_system();
-        *(volatile u64 *)&pub->seq = seq;
+// level on MI355X).  The LAST workgroup of the level's last kernel publishes (a separate one-wave kernel cost ~6-9 us
+// per level: its dependent-dispatch gap plus the kernel).  Every workgroup fences its
+// shard / queue atomics and arrives on the slot's `done` counter; the one that arrives last reads the
+// shards back with device-scope loads (they were updated by device-scope atomics, which bypass the XCD
+// L2s) and writes the record to mapped host memory.  Block-uniform; pub == null: no-op.
+__device__ inline void publish_if_last(LevelSlot *slot, Published *pub, u64 seq) {
+    if (!pub) return;
+    __shared__ int s_last;
+    // hand-off without fences (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1
+    // table): every wave drains its own shard / queue atomics (device-scope atomics are performed at the
+    // memory side), a barrier, then ONE agent-scope add per workgroup whose returned value names the
+    // last arriver, which reads the shards back with sc1 loads.  A __threadfence() here writes back the
+    // XCD's L2 in every workgroup (buffer_wbl2): it doubled the BFS time.
+    // The arrivals are sharded (blockIdx % 8, one line each; the last of a shard adds to `done`): ~1,500
+    // workgroups on one counter queue ~12 ns each at the memory side, which a tail of simultaneous
+    // finishers would pay in full.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned G = gridDim.x, sh = blockIdx.x % kDoneShards;
+        const u64 n_sh = (G - sh + kDoneShards - 1) / kDoneShards; // workgroups of this shard
+        int last = __hip_atomic_fetch_add(&slot->dsh[sh].n, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   n_sh - 1ull;
+        if (last)
+            last = __hip_atomic_fetch_add(&slot->done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (u64)min(G, (unsigned)kDoneShards) - 1ull;
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x < 64) {
+        const unsigned lane = threadIdx.x;
+        const u64 *sh = reinterpret_cast<const u64 *>(&slot->sh[lane]);
+        auto ld = [](const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        const u64 nf = wave_sum(ld(sh + 0)), mf = wave_sum(ld(sh + 1)), sc = wave_sum(ld(sh + 2)),
+                  cl = wave_sum(ld(sh + 3)), mu = wave_sum(ld(sh + 4)), s2 = wave_sum(ld(sh + 5)),
+                  wk = wave_sum(ld(sh + 6)), dmax = wave_max(ld(sh + 7));
+        const u64 qt = ld(&slot->qtail);
+        if (lane == 0) {
+            // mapped host memory (uncached): the record's stores complete before the sequence number's
+            volatile Published *vp = pub;
+            vp->stage2 = (int64_t)s2;
+            vp->walked = (int64_t)wk;
+            vp->qtail = (int64_t)qt;
+            vp->nf = (int64_t)nf;
+            vp->mf = (int64_t)mf;
+            vp->sc = (int64_t)sc;
+            vp->cl = (int64_t)cl;
+            vp->mu = (int64_t)mu;
+            vp->dmax = (int64_t)dmax;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            vp->seq = seq;
+        }
     }
 }
 
@@ -418,7 +461,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
                                             LevelSlot *ring, int level, uint32_t hub_deg,
                                             uint32_t *__restrict__ hubs, Part pt, int gsz, HubSet hs,
-                                            HubSet skip) {
+                                            HubSet skip, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
@@ -482,13 +525,14 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     if (kDist) rq_flush(*rq, pt);
     // top-down: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
+    publish_if_last(cn, pub, seq);
 }
 
 template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  u64 *vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
-                                                 Part pt, HubSet hs) {
+                                                 Part pt, HubSet hs, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
@@ -551,6 +595,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     bq_flush(q, qout, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
+    publish_if_last(cn, pub, seq);
 }
 
 // ---- K3p: persistent top-down for narrow frontiers --------------------------------------------------
@@ -643,7 +688,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
                                                     PersistOut *out, HubSet hs, int64_t bu_floor,
-                                                    int inject_abort) {
+                                                    int inject_abort, u64 dmax_cap) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_scan[kBS + 1];
@@ -861,7 +906,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             out->levels = (u64)(it + 1);
         }
         mu -= (int64_t)mf_new;
-        const bool stop = nf_new == 0 || nf_new > kPersistNf ||
+        const bool stop = nf_new == 0 || nf_new > kPersistNf || dm_new > dmax_cap ||
                           (u64)((nf_new + G - 1) / G) * dm_new > (u64)kRegion ||
                           (alpha > 0 && (int64_t)mf_new > mu / alpha && (int64_t)mf_new > bu_floor) ||
                           it + 1 >= max_levels;
@@ -1061,13 +1106,17 @@ __device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *_
 // row order (the last one repeated for rows shorter than 4, so every slot is a real neighbour) and
 // its degree (saturated at 2^32-1).  A miss on top1 probes c1..c3 at once from this one 16-B load;
 // only rows longer than 4 without a hit there walk their row (phase B, from entry 4).
-template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly>
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6 : 7))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+// kPipe: the next round's top1 loads are issued right after this round's frontier probes, so they
+// overlap the probes, stage A2 and phase B instead of opening the next round (one dependent memory
+// latency fewer per round; a half-group of dense candidates runs up to 8 rounds).
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kPipe ? 5 : (kU == 4 ? 6 : 7)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
-                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim) {
+                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, Published *pub,
+                                            u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
@@ -1108,22 +1157,49 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
                 }
             }
             __builtin_amdgcn_wave_barrier();
+            uint32_t xn[kU]; // kPipe: top1 of the next round's candidates, in flight
+            if (kPipe) {
+#pragma unroll
+                for (int k = 0; k < kU; k++) {
+                    const uint32_t vk = vbase + s_cand[wave][(uint32_t)k * 64 + lane];
+                    xn[k] = (hb + (uint32_t)k * 64 + lane < he) ? top1[vk] : 0u;
+                }
+            }
             for (uint32_t t0 = hb; t0 < he; t0 += (64 * kU)) {
                 uint32_t v[kU], x[kU];
 #pragma unroll
                 for (int k = 0; k < kU; k++) // past the half's end: masked below
                     v[k] = vbase + s_cand[wave][t0 - hb + (uint32_t)k * 64 + lane];
-                __builtin_amdgcn_wave_barrier();
                 // A1: top1 of every candidate, then its frontier bit
+                const uint32_t t1 = t0 + 64 * kU; // next round
+                uint32_t vn[kU];
+                if (kPipe) {
 #pragma unroll
-                for (int k = 0; k < kU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < he) ? top1[v[k]] : 0u;
+                    for (int k = 0; k < kU; k++) {
+                        x[k] = xn[k];
+                        const uint32_t at = t1 - hb + (uint32_t)k * 64 + lane; // past the list: unused (masked below)
+                        vn[k] = vbase + s_cand[wave][at < 2048u ? at : 0u];
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < kU; k++) x[k] = (t0 + (uint32_t)k * 64 + lane < he) ? top1[v[k]] : 0u;
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint32_t pw[kU]; // the 32-bit frontier word of each candidate's top1
+#pragma unroll
+                for (int k = 0; k < kU; k++) {
+                    const uint32_t xx = x[k] & ~fmask;
+                    pw[k] = ((t0 + (uint32_t)k * 64 + lane < he) && (!kHubOnly || hub_entry<kHubs>(xx, hub_lim)))
+                                ? reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, xx))[(xx >> 5) & 1u]
+                                : 0u;
+                }
+                if (kPipe && t1 < he) { // wave-uniform; issued after the probes, so waiting on them does not wait on these
+#pragma unroll
+                    for (int k = 0; k < kU; k++) xn[k] = (t1 + (uint32_t)k * 64 + lane < he) ? top1[vn[k]] : 0u;
+                }
                 uint32_t fbm = 0u; // bit k: candidate k's top1 is in the frontier
 #pragma unroll
-                for (int k = 0; k < kU; k++)
-                    fbm |= ((t0 + (uint32_t)k * 64 + lane < he) && (!kHubOnly || hub_entry<kHubs>(x[k] & ~fmask, hub_lim))
-                                ? probe_bit<kHubs>(front, hfront, x[k] & ~fmask)
-                                : 0u)
-                           << k;
+                for (int k = 0; k < kU; k++) fbm |= ((pw[k] >> ((x[k] & ~fmask) & 31u)) & 1u) << k;
                 // A2: misses of A1 load rest[v] (c1..c3 + degree) and probe c1..c3 together
                 uint4 r[kU];
 #pragma unroll
@@ -1245,6 +1321,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kU == 4 ? 6
     }
     // claims field: rows walked (phase B)
     shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk);
+    publish_if_last(cn, pub, seq);
 }
 
 // ---- K4: frontier representation changes -------------------------------------------------------
@@ -1257,12 +1334,15 @@ __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restr
 
 // The same with the queue length read on the device (the top-down half of a hybrid level appends to
 // the queue; its length is known to the host only after the level is published).
-__global__ __launch_bounds__(kBS) void k_queue_to_bitmap_dev(const uint32_t *__restrict__ q, const u64 *qlen, u64 *bm) {
-    const uint32_t n = (uint32_t)*qlen;
+// Publishes the level (hybrid levels end with it).
+__global__ __launch_bounds__(kBS) void k_queue_to_bitmap_dev(const uint32_t *__restrict__ q, LevelSlot *cn, u64 *bm,
+                                                             Published *pub, u64 seq) {
+    const uint32_t n = (uint32_t)cn->qtail;
     for (uint32_t i = blockIdx.x * kBS + threadIdx.x; i < n; i += gridDim.x * kBS) {
         const uint32_t v = q[i];
         atomicOr(bm + (v >> 6), 1ull << (v & 63u));
     }
+    publish_if_last(cn, pub, seq);
 }
 
 // Frontier of a top-down level as a bitmap without one atomic per vertex: the visited bitmap after
@@ -1489,7 +1569,7 @@ __global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, cons
 }
 
 // Multi-GPU host reads without a D2H copy + stream synchronise: one wave copies two device ranges into
-// mapped pinned host memory and then publishes a sequence number the host spins on (as k_publish).
+// mapped pinned host memory and then publishes a sequence number the host spins on (as publish_if_last).
 __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict__ b, int nb, u64 *post, u64 seq) {
     for (int i = threadIdx.x; i < na + nb; i += blockDim.x) post[1 + i] = i < na ? a[i] : b[i - na];
     __threadfence_system();
@@ -1720,9 +1800,10 @@ bool has_hubs(const BfsWorkspace *ws) { return ws->hub_k > 0 || ws->hub_lim > 0;
 // dmax: largest degree in the frontier (< 0: unknown) -- the hub bin is skipped when no vertex exceeds
 // the hub degree
 // skip_hubs (hybrid level): frontier vertices of the hub domain are left to the bottom-up hub sweep.
+// pub != null: the last kernel launched publishes the level's counters (seq) from its last workgroup
 template <bool kDist>
 int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt,
-              bool skip_hubs = false) {
+              bool skip_hubs = false, Published *pub = nullptr, u64 seq = 0) {
     hipStream_t st = g->ctx->stream;
     const HubSet hs = hub_set(ws);
     const HubSet skip = skip_hubs ? hs : HubSet{0xFFFFFFFFu, 0u};
@@ -1736,34 +1817,38 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip);
+                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip,
+                           hubs ? nullptr : pub, seq);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs);
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs, pub, seq);
             BFSX_HIP_TRY(hipGetLastError());
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip);
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip,
+                           hubs ? nullptr : pub, seq);
         BFSX_HIP_TRY(hipGetLastError());
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs);
+                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs, pub, seq);
             BFSX_HIP_TRY(hipGetLastError());
         }
     }
     return BFSX_OK;
 }
 
-template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly>
-int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
+int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
+                u64 seq) {
     hipStream_t st = g->ctx->stream;
     // persistent grid: exactly the resident workgroups (a partial second wave of workgroups would
     // leave most CUs idle at the tail of the grid-stride loop)
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs, kU, kHubOnly>, kBS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>, kBS, 0) !=
+                hipSuccess ||
             per_cu < 1)
             per_cu = 4;
     }
@@ -1774,42 +1859,44 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
                            ws->hub_id, ws->hub_k, front, ws->hfront);
         BFSX_HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
+    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
                        ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
-                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim);
+                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, pub, seq);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
 
 template <class OffT, bool kMf, bool kHubs>
-int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level) {
-    return g->ctx->opt.bu_unroll == 2 ? launch_bu_u<OffT, kMf, kHubs, 2, false>(g, ws, row_off, front, level)
-                                      : launch_bu_u<OffT, kMf, kHubs, 4, false>(g, ws, row_off, front, level);
+int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
+                u64 seq) {
+    if (g->ctx->opt.bu_unroll == 2) return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, level, pub, seq);
+    return g->ctx->opt.bu_pipeline ? launch_bu_u<OffT, kMf, kHubs, 4, false, true>(g, ws, row_off, front, level, pub, seq)
+                                   : launch_bu_u<OffT, kMf, kHubs, 4, false, false>(g, ws, row_off, front, level, pub, seq);
 }
 
 // The bottom-up half of a hybrid level: candidates probe only the hubs of the frontier (single device).
 int launch_bu_hubonly(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
     if (ws->hub_k > 0)
-        return ws->off32 ? launch_bu_u<uint32_t, false, true, 4, true>(g, ws, ws->off32, front, level)
-                         : launch_bu_u<int64_t, false, true, 4, true>(g, ws, g->d_row_off, front, level);
-    return ws->off32 ? launch_bu_u<uint32_t, false, false, 4, true>(g, ws, ws->off32, front, level)
-                     : launch_bu_u<int64_t, false, false, 4, true>(g, ws, g->d_row_off, front, level);
+        return ws->off32 ? launch_bu_u<uint32_t, false, true, 4, true, false>(g, ws, ws->off32, front, level, nullptr, 0)
+                         : launch_bu_u<int64_t, false, true, 4, true, false>(g, ws, g->d_row_off, front, level, nullptr, 0);
+    return ws->off32 ? launch_bu_u<uint32_t, false, false, 4, true, false>(g, ws, ws->off32, front, level, nullptr, 0)
+                     : launch_bu_u<int64_t, false, false, 4, true, false>(g, ws, g->d_row_off, front, level, nullptr, 0);
 }
 
 template <bool kMf>
-int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
+int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level, Published *pub = nullptr, u64 seq = 0) {
     if (ws->hub_k > 0) // top1 is hub-encoded: every bottom-up launch of this graph uses the hub domain
-        return ws->off32 ? launch_bu_t<uint32_t, kMf, true>(g, ws, ws->off32, front, level)
-                         : launch_bu_t<int64_t, kMf, true>(g, ws, g->d_row_off, front, level);
-    return ws->off32 ? launch_bu_t<uint32_t, kMf, false>(g, ws, ws->off32, front, level)
-                     : launch_bu_t<int64_t, kMf, false>(g, ws, g->d_row_off, front, level);
+        return ws->off32 ? launch_bu_t<uint32_t, kMf, true>(g, ws, ws->off32, front, level, pub, seq)
+                         : launch_bu_t<int64_t, kMf, true>(g, ws, g->d_row_off, front, level, pub, seq);
+    return ws->off32 ? launch_bu_t<uint32_t, kMf, false>(g, ws, ws->off32, front, level, pub, seq)
+                     : launch_bu_t<int64_t, kMf, false>(g, ws, g->d_row_off, front, level, pub, seq);
 }
 
 struct SlotSums {
     int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0;
 };
 
-// Spin until k_publish of the current sequence number has landed; poll the stream now and then so a
+// Spin until the level's counters of the current sequence number have landed; poll the stream now and then so a
 // faulted kernel surfaces as an error instead of a hang.
 int wait_published(BfsWorkspace *ws, hipStream_t st) {
     const volatile u64 *seq = &ws->h_pub->seq;
@@ -1879,8 +1966,12 @@ int persist_blocks(const bfsx_ctx *ctx) {
 // Whether a top-down level of nf vertices (largest degree dmax, < 0: unknown) may start K3p: every
 // workgroup's slice must fit its output segment whatever it discovers.  G is the grid the launch will
 // use: fixed at the graph's first K3p launch (ws->persist_grid), the option's value before it.
+// A frontier vertex's row is swept by ONE workgroup of K3p (kBS * kItems entries per dependent step), so a
+// frontier holding a vertex of degree > persist_dmax goes to the per-level kernels, whose multi-workgroup
+// hub bin spreads that row over the whole grid (a 5,000-entry row took 52 us in K3p, ~20 us per level).
 bool persist_fits(const bfsx_ctx *ctx, const BfsWorkspace *ws, int64_t nf, int64_t dmax) {
     if (!ctx->opt.persist || ws->persist_off || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
+    if (dmax > ctx->opt.persist_dmax) return false;
     const int64_t G = ws->persist_seg ? ws->persist_grid : persist_blocks(ctx);
     if (G < 1) return false;
     return ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
@@ -1946,12 +2037,12 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           hub_set(ws), bu_floor(ws), opt.persist_abort_at);
+                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           hub_set(ws), bu_floor(ws), opt.persist_abort_at);
+                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -2094,11 +2185,10 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             const Part pt{};
             if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true)) return e; // -> qb
             LevelSlot *cn = ws->ring + (level + 1) % 3;
-            hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, &cn->qtail, ws->next);
+            hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, cn, ws->next, ws->d_pub,
+                               ++ws->pub_seq);
             BFSX_HIP_TRY(hipGetLastError());
             BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-            hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, cn, ws->d_pub, ++ws->pub_seq);
-            BFSX_HIP_TRY(hipGetLastError());
             if (int e = wait_published(ws, st)) return e;
             const int64_t nf_new = ws->h_pub->nf + ws->h_pub->qtail;
             g->level_dirs.push_back(BFSX_DIR_HYBRID);
@@ -2199,15 +2289,13 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                 snapped = true;
             }
             const Part pt{};
-            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt)) return e;
+            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, false, ws->d_pub, ++ws->pub_seq)) return e;
             td_levels++;
         } else {
-            if (int e = launch_bu<false>(g, ws, ws->front, level)) return e;
+            if (int e = launch_bu<false>(g, ws, ws->front, level, ws->d_pub, ++ws->pub_seq)) return e;
             bu_levels++;
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-        hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, ws->d_pub, ++ws->pub_seq);
-        BFSX_HIP_TRY(hipGetLastError());
         if (int e = wait_published(ws, st)) return e;
         SlotSums s;
         s.nf = ws->h_pub->nf;

@@ -99,6 +99,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
  *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU, capped by the occupancy API so
  *                 that every workgroup is resident; fixed at a graph's first BFS)
+ *   "persist_dmax" = int (the persistent launch runs only while every frontier vertex has at most this
+ *                 degree; a heavier row is spread over the whole grid by the per-level kernels; default 2048)
  *   "persist_abort_at" = int|off (test hook: that persistent launch aborts at its k-th level as a barrier
  *                 timeout would; the BFS is then re-run without it; default off)
  *   "hub_bits" = auto|off|1..30 (bottom-up probes of the 2^b highest-degree vertices go to a small
@@ -106,6 +108,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "hybrid" = auto|off|force (a top-down level whose frontier's edges sit mostly in hub-domain vertices
  *                 runs as pull-from-hubs + push-from-the-rest; force = every eligible level, for tests)
  *   "bu_unroll" = 4|2 (bottom-up candidates per lane per round)
+ *   "bu_pipeline" = on|off (bottom-up: the next round's first-neighbour loads overlap the current round;
+ *                 with bu_unroll 4; default on)
  *   "slot_pairs" = int (partitioned graphs: a push level whose frontier has at most this many edges in
  *                 total exchanges its pairs through fixed per-peer slots, skipping the count all-to-all
  *                 and its host wait; default 16384, 0 = never)

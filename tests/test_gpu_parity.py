@@ -444,11 +444,14 @@ def test_chunked_csr_build(ctx, chunk, relabel):
         ctx.set_option("relabel", "on")
 
 
-@pytest.mark.parametrize("unroll", ["2", "4"])
-def test_bottomup_unroll_variants(ctx, unroll):
-    """Both k_bu instantiations (2 or 4 candidates per lane per round) are bit-exact, pull-only and
-    direction-optimising, with and without the hub probe domain."""
-    ctx.set_option("bu_unroll", unroll)
+@pytest.mark.parametrize("relabel", ["on", "off"])
+@pytest.mark.parametrize("unroll", ["2", "4", "4-nopipe"])
+def test_bottomup_unroll_variants(ctx, unroll, relabel):
+    """Every k_bu instantiation (2 or 4 candidates per lane per round; with 4, the next round's top1
+    loads pipelined or not) is bit-exact, pull-only and direction-optimising, with and without hubs."""
+    ctx.set_option("bu_unroll", unroll.split("-")[0])
+    ctx.set_option("bu_pipeline", "off" if unroll.endswith("nopipe") else "on")
+    ctx.set_option("relabel", relabel)
     try:
         for hub in ("off", "auto"):
             ctx.set_option("hub_bits", hub)
@@ -466,7 +469,8 @@ def test_bottomup_unroll_variants(ctx, unroll):
                     for r in g.sample_roots(2, seed=4):
                         check_against_oracle(g, 1 << 16, off, col, int(r), ou, ov, mr=False)
     finally:
-        for k, val in (("bu_unroll", "4"), ("hub_bits", "auto"), ("direction", "auto")):
+        for k, val in (("bu_unroll", "4"), ("bu_pipeline", "on"), ("relabel", "on"), ("hub_bits", "auto"),
+                       ("direction", "auto")):
             ctx.set_option(k, val)
 
 
