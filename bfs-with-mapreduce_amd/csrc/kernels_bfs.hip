@@ -1110,7 +1110,7 @@ __device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *_
 // overlap the probes, stage A2 and phase B instead of opening the next round (one dependent memory
 // latency fewer per round; a half-group of dense candidates runs up to 8 rounds).
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kPipe ? 5 : (kU == 4 ? 6 : 7)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 6 : (kU == 4 ? 5 : 6)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
@@ -1870,8 +1870,11 @@ template <class OffT, bool kMf, bool kHubs>
 int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
                 u64 seq) {
     if (g->ctx->opt.bu_unroll == 2) return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, level, pub, seq);
-    return g->ctx->opt.bu_pipeline ? launch_bu_u<OffT, kMf, kHubs, 4, false, true>(g, ws, row_off, front, level, pub, seq)
-                                   : launch_bu_u<OffT, kMf, kHubs, 4, false, false>(g, ws, row_off, front, level, pub, seq);
+    // kMf (partitioned) + kPipe needs more than the 96 VGPRs of 5 waves per SIMD: it would spill, so the
+    // partitioned pull level runs unpipelined
+    return g->ctx->opt.bu_pipeline && !kMf
+               ? launch_bu_u<OffT, kMf, kHubs, 4, false, !kMf>(g, ws, row_off, front, level, pub, seq)
+               : launch_bu_u<OffT, kMf, kHubs, 4, false, false>(g, ws, row_off, front, level, pub, seq);
 }
 
 // The bottom-up half of a hybrid level: candidates probe only the hubs of the frontier (single device).

@@ -31,6 +31,6 @@ def run(opts, world=4, scale=20, roots=2):
 
 import sys
 for world in (1, 2, 4):
-    for opts in ({}, {"direction": "bottomup"}):
+    for opts in ({}, {"direction": "bottomup"}, {"hub_bits": "off"}):
         r = run(opts, world=world)
         print(world, opts, [(s, e) for s, e, _ in r], flush=True)
