@@ -250,13 +250,18 @@ int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t s
 }
 
 // Row chunks [cuts[i], cuts[i+1]) of at most `limit` entries each (a longer single row is a chunk of
-// its own), from a host copy of the offsets.
+// its own) and at most kChunkRows rows, from a host copy of the offsets.  The row cap: rocPRIM's
+// segmented radix sort mis-sorts chunks of very many tiny segments (a relabelled scale-29/30 graph's
+// tail chunk: 2^30 entries in hundreds of millions of rows of degree 1..7 moved entries between rows,
+// `profiles/r02i_segsort.txt`); 2^24 rows per chunk stays far below that.
+constexpr int64_t kChunkRows = (int64_t)1 << 24;
 int plan_row_chunks(const std::vector<int64_t> &h_off, int64_t nv, int64_t limit, std::vector<int64_t> &cuts) {
     cuts.assign(1, 0);
     int64_t r = 0;
     while (r < nv) {
         int64_t r2 = std::upper_bound(h_off.begin() + r, h_off.begin() + nv + 1, h_off[r] + limit) - h_off.begin() - 1;
         if (r2 <= r) r2 = r + 1; // one row longer than the limit
+        r2 = std::min<int64_t>(r2, r + kChunkRows);
         if (h_off[r2] - h_off[r] >= ((int64_t)1 << 31)) return fail(BFSX_E_ARG, "a single adjacency row exceeds 2^31 entries");
         r2 = std::min<int64_t>(r2, nv);
         cuts.push_back(r2);
