@@ -5,7 +5,7 @@ set -e -o pipefail
 TAG=$1; RE=$2
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-p1"
 i=0
 MODE=${3:-default}
 if [ "$MODE" = "sq" ]; then
