@@ -154,15 +154,25 @@ int load_algs4_device(bfsx_ctx *ctx, const char *path, int64_t &nv, int64_t &m, 
 
 } // namespace
 
-// Original vertex id -> the internal id every device array is indexed by (identity without relabel).
+// Original vertex id -> the global internal id every device array is indexed by (identity without
+// relabel).  v must be owned by this rank (the relabel keeps every id inside its owner's range).
 int to_internal(const bfsx_graph *g, int64_t v, int64_t *out) {
     if (!g->d_perm) {
         *out = v;
         return BFSX_OK;
     }
+    if (v < g->v_lo || v >= g->v_lo + g->nv) return fail(BFSX_E_ARG, "vertex not owned by this rank");
     uint32_t x = 0;
-    BFSX_HIP_TRY(hipMemcpy(&x, g->d_perm + v, sizeof(x), hipMemcpyDeviceToHost));
-    *out = (int64_t)x;
+    BFSX_HIP_TRY(hipMemcpy(&x, g->d_perm + (v - g->v_lo), sizeof(x), hipMemcpyDeviceToHost));
+    *out = g->v_lo + (int64_t)x;
+    return BFSX_OK;
+}
+
+// A relabelled partition's source as the validator sees it (dist_begin's convention): its global
+// internal id on the owner, nv_global (no row) on the other ranks -- no collective needed.
+int dist_map_source(const bfsx_graph *g, int64_t source, int64_t *out) {
+    if (source >= g->v_lo && source < g->v_lo + g->nv) return to_internal(g, source, out);
+    *out = g->nv_global;
     return BFSX_OK;
 }
 
@@ -398,14 +408,15 @@ static bfsx_graph *new_partition(bfsx_ctx *ctx, int64_t nv, int64_t m, int rank,
     return g;
 }
 
-// dist: built for the partitioned loop (bfsx_dist_*), which runs on original ids even at one rank (the
-// relabel is a single-device layout; a partition would hand every hub to rank 0)
+// dist: built for the partitioned loop (bfsx_dist_*).  The relabel renumbers inside every rank's id
+// range (ranges of `chunk` ids; one range on one device), so ownership never changes.
 static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uint32_t *d_v, int64_t m, int rank,
                                    int nranks, bfsx_graph **out, bool dist) {
     bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
     if (!g) return fail(BFSX_E_OOM, "graph");
     set_build_chunk(ctx->opt.build_chunk);
-    int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, ctx->opt.relabel && !dist,
+    (void)dist;
+    int rc = build_csr_device(ctx->stream, g->nv, d_u, d_v, m, ctx->opt.degree_order, ctx->opt.relabel ? g->chunk : 0,
                               &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt, &g->d_perm, &g->d_inv, g->v_lo, nv);
     if (rc) {
         delete g;
@@ -527,8 +538,9 @@ static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t se
     bfsx_graph *g = new_partition(ctx, nv, m, rank, nranks);
     if (!g) return fail(BFSX_E_OOM, "graph");
     set_build_chunk(ctx->opt.build_chunk);
+    (void)dist;
     int rc = build_csr_kronecker(ctx->stream, scale, edgefactor, seed, ctx->opt.degree_order,
-                                 ctx->opt.relabel && !dist, &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt,
+                                 ctx->opt.relabel ? g->chunk : 0, &g->d_row_off, &g->d_col, &g->nnz, &g->d_tuple_cnt,
                                  &g->d_perm, &g->d_inv, g->v_lo, g->nv);
     (void)hipStreamSynchronize(ctx->stream);
     if (rc) {
@@ -767,6 +779,9 @@ int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first
     if (source >= 0 && g->nranks == 1) {
         if (source >= g->nv) return fail(BFSX_E_ARG, "source out of range");
         if (int rc = to_internal(g, source, &si)) return rc;
+    } else if (source >= 0 && g->d_perm) { // relabelled partition: the owner maps the source (collective)
+        if (source >= g->nv_global) return fail(BFSX_E_ARG, "source out of range");
+        if (int rc = dist_map_source(g, source, &si)) return rc;
     }
     if (int rc = bfs_validate(g, si, nullptr, res)) return rc;
     if (int rc = to_original(g, res[1], &res[1])) return rc;
@@ -780,6 +795,7 @@ int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first
 int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, const int64_t *parent, int64_t *errors,
                          int64_t *first_bad) {
     if (!g || !dist || !parent) return fail(BFSX_E_ARG, "null argument");
+    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: use bfsx_validate (collective)");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     std::vector<unsigned long long> packed((size_t)g->nv);
     std::vector<uint32_t> perm;

@@ -33,7 +33,7 @@ struct Options {
     int persist_blocks = 0;     // K3p workgroups (0: one per CU)
     int offset_bits = 0;        // traversal row-offset width: 0 = uint32 when nnz < 2^32, else int64; 64 = int64
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)
-    bool relabel = true;        // single-device graphs: vertices renumbered by degree (desc) at build
+    bool relabel = true;        // vertices renumbered by degree (desc) at build, inside every rank's id range
     int hub_bits = -1;          // bottom-up hub probe domain: -1 auto, 0 off, b = 2^b hubs
     int bu_unroll = 4;          // bottom-up candidates per lane per round (4 or 2)
     bool bu_pipeline = true;    // bottom-up: the next round's top1 loads overlap this round (kU = 4)
@@ -61,10 +61,12 @@ struct Comm {
 // arrays.  Takes ownership of nothing; d_u/d_v stay owned by the caller.
 // Rows are built for the global id range [lo, lo + nv) only (lo = 0, nv = all for one device);
 // nv_global sizes the sort keys and the degree table of the degree-ordered rows.
-// relabel (single-device graphs with degree_order only): vertices renumbered by degree, descending;
-// *d_perm (original -> internal) and *d_inv (internal -> original) are set, else left untouched.
+// relabel_chunk > 0 (with degree_order): vertices renumbered by degree, descending, inside every id range
+// [r*relabel_chunk, (r+1)*relabel_chunk) (one range on one device, the ranks' ranges on a partition);
+// *d_perm = this rank's slice of the permutation (local internal row of original local id i) and
+// *d_inv = the whole inverse (original id of global internal id x) are set, else left untouched.
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
-                     bool degree_order, bool relabel, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
+                     bool degree_order, int64_t relabel_chunk, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
                      uint32_t **d_tuple_cnt, uint32_t **d_perm, uint32_t **d_inv, int64_t lo = 0,
                      int64_t nv_global = -1);
 // Row-chunk size (raw adjacency entries) of the CSR build's sort/dedup/ordering passes, calling thread.
@@ -77,9 +79,9 @@ int kronecker_generate(hipStream_t stream, int scale, int edgefactor, uint64_t s
 int parse_algs4_device(hipStream_t st, const char *body, size_t n, int64_t nv, int64_t first_lineno, uint32_t **d_u,
                        uint32_t **d_v, int64_t *m);
 // The same CSR built straight from the Kronecker counter stream (rows of global ids [lo, lo+nv_local)).
-int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order, bool relabel,
-                        int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, uint32_t **d_perm,
-                        uint32_t **d_inv, int64_t lo, int64_t nv_local);
+int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order,
+                        int64_t relabel_chunk, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
+                        uint32_t **d_tuple_cnt, uint32_t **d_perm, uint32_t **d_inv, int64_t lo, int64_t nv_local);
 
 // D2H copy of a relabelled graph's CSR in ORIGINAL ids (rows of original ids, entries mapped back;
 // each row keeps its degree-descending order).  row_off[nv+1] / col[nnz] host, either may be null.
@@ -131,7 +133,7 @@ struct bfsx_graph {
     int64_t *d_row_off = nullptr; // [nv+1]
     uint32_t *d_col = nullptr;    // [nnz]
     uint32_t *d_tuple_cnt = nullptr; // [nv]: input tuples whose first endpoint is v (m_comp)
-    // degree-descending relabel (single device, option "relabel"): every device array is indexed by the
+    // degree-descending relabel (option "relabel", inside every rank's id range): every device array is indexed by the
     // internal id; perm[original] = internal, inv[internal] = original.  Null: internal = original.
     uint32_t *d_perm = nullptr, *d_inv = nullptr;
     bfsx::BfsWorkspace *ws = nullptr;

@@ -1429,13 +1429,14 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, int
     }
 }
 
-// The same for a relabelled graph: internal row i is original vertex inv[i]; parents map back too.
+// The same for a relabelled graph: internal local row i is original vertex inv[lo + i] (a partition's
+// relabel keeps it inside the rank's range [lo, lo + n)); parents are global internal ids and map back too.
 __global__ __launch_bounds__(kBS) void k_unpack_relabel(const u64 *__restrict__ stt, const uint32_t *__restrict__ inv,
-                                                        int64_t n, int32_t *__restrict__ dist,
+                                                        int64_t lo, int64_t n, int32_t *__restrict__ dist,
                                                         int32_t *__restrict__ parent) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
         const u64 s = stt[i];
-        const uint32_t o = inv[i], p = (uint32_t)(s >> 32);
+        const uint32_t o = (uint32_t)((int64_t)inv[lo + i] - lo), p = (uint32_t)(s >> 32);
         dist[o] = (int32_t)(uint32_t)s;
         parent[o] = p == 0xFFFFFFFFu ? -1 : (int32_t)inv[p];
     }
@@ -1487,11 +1488,14 @@ __global__ __launch_bounds__(kBS) void k_rest(const int64_t *__restrict__ row_of
     }
 }
 
-// Degrees of this rank's rows as uint32, padded with 0 to `chunk` entries (the all-gather slice).
-__global__ __launch_bounds__(kBS) void k_slice_degrees(const int64_t *__restrict__ row_off, int64_t nv, int64_t chunk,
-                                                       uint32_t *__restrict__ out) {
-    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < chunk; v += (int64_t)gridDim.x * kBS)
-        out[v] = v < nv ? (uint32_t)(row_off[v + 1] - row_off[v]) : 0u;
+// Degrees of this rank's rows as uint32, padded with 0 to `chunk` entries (the all-gather slice); with
+// `perm` (a relabelled partition's slice of the permutation) in ORIGINAL id order.
+__global__ __launch_bounds__(kBS) void k_slice_degrees(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ perm,
+                                                       int64_t nv, int64_t chunk, uint32_t *__restrict__ out) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < chunk; v += (int64_t)gridDim.x * kBS) {
+        const int64_t r = (perm && v < nv) ? (int64_t)perm[v] : v;
+        out[v] = v < nv ? (uint32_t)(row_off[r + 1] - row_off[r]) : 0u;
+    }
 }
 // Hub selection: sort keys ~degree (ascending = degree descending, ties by id: the sort is stable).
 __global__ __launch_bounds__(kBS) void k_hub_keys(const uint32_t *__restrict__ deg, int64_t n,
@@ -1615,6 +1619,7 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     const bool part = g->nranks > 1;
     if (hb == 0 || g->nv_global < 64) return BFSX_OK;
     if (g->d_perm) { // relabelled: hubs = the first k ids (the k highest degrees), nothing to build
+        if (part) return BFSX_OK; // a partition's ranges each start with their hubs; no hybrid levels there
         int64_t k = 64;
         if (hb < 0) {
             if (g->nv < ((int64_t)1 << 16)) return BFSX_OK;
@@ -1653,12 +1658,12 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     const unsigned gfill = clamp_grid(((int64_t)nr + kBS - 1) / kBS, 8192);
     if (part) {
         BFSX_HIP_TRY(hipMalloc(&slice.p, (size_t)g->chunk * sizeof(uint32_t)));
-        hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, g->chunk,
+        hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, nullptr, g->nv, g->chunk,
                            (uint32_t *)slice.p);
         BFSX_HIP_TRY(hipGetLastError());
         if (int e = cm->allgather((const u64 *)slice.p, g->chunk / 2, (u64 *)degs.p, st)) return e;
     } else {
-        hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, g->nv,
+        hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, nullptr, g->nv, g->nv,
                            (uint32_t *)degs.p);
         BFSX_HIP_TRY(hipGetLastError());
     }
@@ -2407,7 +2412,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     int32_t *d_dist = reinterpret_cast<int32_t *>(ws->qa), *d_par = reinterpret_cast<int32_t *>(ws->qb);
     if (g->d_inv)
         hipLaunchKernelGGL(k_unpack_relabel, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                           ws->st, g->d_inv, (int64_t)nv, d_dist, d_par);
+                           ws->st, g->d_inv, g->v_lo, (int64_t)nv, d_dist, d_par);
     else
         hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
                            (int64_t)nv, d_dist, d_par);
@@ -2479,7 +2484,12 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
     BfsWorkspace *ws = g->ws;
     hipStream_t st = g->ctx->stream;
     const bool owned = source >= g->v_lo && source < g->v_lo + g->nv;
-    const int64_t sl = owned ? source - g->v_lo : -1;
+    int64_t sl = owned ? source - g->v_lo : -1; // local internal row of the source
+    if (owned && g->d_perm) {
+        uint32_t x = 0;
+        BFSX_HIP_TRY(hipMemcpy(&x, g->d_perm + sl, sizeof(x), hipMemcpyDeviceToHost));
+        sl = (int64_t)x;
+    }
     int64_t deg = 0;
     if (owned && deg_known >= 0) {
         deg = deg_known;
@@ -2491,7 +2501,7 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                       owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)source, ws->prev_source, ws->dead, ws->nwords,
+                       owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)(g->v_lo + sl), ws->prev_source, ws->dead, ws->nwords,
                        ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_HIP_TRY(hipGetLastError());
     ws->prev_source = sl;
@@ -2503,7 +2513,9 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
     g->level_dirs.clear();
     g->level_cum_ms.clear();
     g->level_stats.clear();
-    g->last_source = source;
+    // the result's source as the validator sees it: its global internal id on the owner; on the other
+    // ranks of a relabelled partition nv_global, which names no row (only the owner knows the mapping)
+    g->last_source = (owned || !g->d_perm) ? (owned ? g->v_lo + sl : source) : g->nv_global;
     *deg_local = deg;
     return BFSX_OK;
 }
@@ -2737,7 +2749,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         BFSX_HIP_TRY(hipMalloc(&slice, g->chunk * sizeof(uint32_t)));
         BFSX_HIP_TRY(hipMalloc(&all, ng * sizeof(uint32_t)));
         hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                           g->d_row_off, g->nv, g->chunk, reinterpret_cast<uint32_t *>(slice));
+                           g->d_row_off, g->d_perm, g->nv, g->chunk, reinterpret_cast<uint32_t *>(slice));
         int e = hipGetLastError() == hipSuccess ? cm->allgather(slice, g->chunk / 2, all, st) : BFSX_E_HIP;
         if (!e) {
             ws->h_gdeg.resize(ng);
@@ -2753,7 +2765,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         }
     }
     if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
-    const int64_t deg = ws->h_gdeg[source]; // global ids index the padded slices directly (v_lo = rank * chunk)
+    const int64_t deg = ws->h_gdeg[source]; // original ids index the padded slices directly (v_lo = rank * chunk)
     int64_t deg_local = 0;
     if ((rc = dist_begin(g, source, &deg_local, deg))) return rc;
 

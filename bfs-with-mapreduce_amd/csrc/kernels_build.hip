@@ -472,12 +472,13 @@ int build_rows(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_o
     return BFSX_OK;
 }
 
-// Degree-descending relabel keys: ~degree (so an ascending sort puts the highest degree first), ids.
-__global__ __launch_bounds__(kBS) void k_rank_keys(const uint32_t *__restrict__ deg, int64_t n,
+// Degree-descending relabel keys of ids [base, base + n): ~degree (an ascending sort puts the highest
+// degree first), ids.
+__global__ __launch_bounds__(kBS) void k_rank_keys(const uint32_t *__restrict__ deg, int64_t base, int64_t n,
                                                    uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
-    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < n; v += (int64_t)gridDim.x * kBS) {
-        keys[v] = ~deg[v];
-        ids[v] = (uint32_t)v;
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        keys[i] = ~deg[base + i];
+        ids[i] = (uint32_t)(base + i);
     }
 }
 
@@ -486,57 +487,91 @@ __global__ __launch_bounds__(kBS) void k_invert(const uint32_t *__restrict__ inv
         perm[inv[i]] = (uint32_t)i;
 }
 
-// Single-device graphs (lo = 0, nv = nv_global) with relabel: the vertices are renumbered by degree,
-// descending (tuple-endpoint degree: duplicates counted, a self-loop once; ties by id), and the CSR is
-// built from the renamed tuples.  Internal id order is then degree order, so
-//   - rows sorted ascending by internal id ARE degree-ordered (no second sort of the adjacency);
-//   - the high-degree vertices every pull probe and push claim concentrates on occupy the first
-//     lines of the frontier / visited bitmaps, the state array and top1/rest (cache-resident), and
-//     the "hubs" of the hybrid levels are simply the ids below a limit;
-//   - isolated vertices sit at the end, in whole words the pull kernel skips with one branch.
-// perm[original] = internal, inv[internal] = original; the C-ABI maps sources and results through them.
+// out[i] = perm[lo + i] - lo: a rank's own slice of the permutation, as local row indices
+__global__ __launch_bounds__(kBS) void k_local_perm(const uint32_t *__restrict__ perm, int64_t lo, int64_t n,
+                                                    uint32_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS)
+        out[i] = (uint32_t)((int64_t)perm[lo + i] - lo);
+}
+
+// Relabel (rchunk > 0): the vertices are renumbered by degree, descending (tuple-endpoint degree:
+// duplicates counted, a self-loop once; ties by id) INSIDE every id range [r*rchunk, (r+1)*rchunk) --
+// one range on a single device, the ranks' ranges on a 1-D partition, so a vertex keeps its owner and
+// a partition's routing (owner = id / chunk) is unchanged -- and the CSR is built from the renamed
+// tuples.  Internal id order is then degree order within every range, so
+//   - the high-degree vertices every pull probe and push claim concentrates on occupy the first lines
+//     of every range of the frontier / visited bitmaps, the state array and top1/rest (cache-resident),
+//     and the "hubs" of the hybrid levels (single device) are simply the ids below a limit;
+//   - on one device, rows sorted ascending by internal id ARE degree-ordered (no second sort of the
+//     adjacency); a partition still degree-orders its rows (their entries span every range);
+//   - isolated vertices sit at the end of their range, in whole words the pull kernel skips.
+// Every rank computes the whole permutation itself from the tuple stream (no exchange).  Returned:
+// *d_perm_out[i] = local internal row of ORIGINAL local id lo + i (a slice of the permutation),
+// *d_inv_out[x] = original id of GLOBAL internal id x (the whole inverse: parents map back through it).
 template <class Src>
-int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_order, bool relabel,
+int build_csr_impl(hipStream_t stream, int64_t nv, Src src, int64_t m, bool degree_order, int64_t rchunk,
                    int64_t **d_row_off_out, uint32_t **d_col_out, int64_t *nnz_out, uint32_t **d_tuple_cnt_out,
                    uint32_t **d_perm_out, uint32_t **d_inv_out, int64_t lo, int64_t nv_global) {
     if (nv_global < 0) nv_global = nv;
-    if (!relabel || lo != 0 || nv != nv_global || !degree_order)
+    if (rchunk <= 0 || !degree_order)
         return build_rows(stream, nv, src, m, degree_order, d_row_off_out, d_col_out, nnz_out, d_tuple_cnt_out, lo,
                           nv_global);
+    const int64_t n = nv_global;
+    const bool single = lo == 0 && nv == n;
     DevBuf<uint32_t> perm, inv;
     {
-        DevBuf<uint32_t> deg, tcnt, keys, keys2, ids;
-        BFSX_HIP_TRY(deg.alloc(nv + 1));
-        BFSX_HIP_TRY(tcnt.alloc(nv));
-        BFSX_HIP_TRY(hipMemsetAsync(deg.p, 0, (nv + 1) * sizeof(uint32_t), stream));
-        BFSX_HIP_TRY(hipMemsetAsync(tcnt.p, 0, nv * sizeof(uint32_t), stream));
+        DevBuf<uint32_t> deg, keys, keys2, ids;
+        BFSX_HIP_TRY(deg.alloc(n + 1));
+        BFSX_HIP_TRY(hipMemsetAsync(deg.p, 0, (n + 1) * sizeof(uint32_t), stream));
         if (m > 0) {
-            hipLaunchKernelGGL(k_count<Src>, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, src, m, 0u, (uint32_t)nv,
-                               deg.p, tcnt.p);
+            hipLaunchKernelGGL(k_count_all<Src>, dim3(grid_for(m, kBS)), dim3(kBS), 0, stream, src, m, deg.p);
             BFSX_HIP_TRY(hipGetLastError());
         }
-        tcnt.reset();
-        BFSX_HIP_TRY(keys.alloc(nv));
-        BFSX_HIP_TRY(keys2.alloc(nv));
-        BFSX_HIP_TRY(ids.alloc(nv));
-        BFSX_HIP_TRY(inv.alloc(nv));
-        hipLaunchKernelGGL(k_rank_keys, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, deg.p, nv, keys.p, ids.p);
-        BFSX_HIP_TRY(hipGetLastError());
-        size_t tb = 0;
-        BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys.p, keys2.p, ids.p, inv.p, (size_t)nv, 0, 32, stream));
+        const int64_t rmax = std::min(rchunk, n);
+        BFSX_HIP_TRY(keys.alloc(rmax));
+        BFSX_HIP_TRY(keys2.alloc(rmax));
+        BFSX_HIP_TRY(ids.alloc(rmax));
+        BFSX_HIP_TRY(inv.alloc(n));
         DevBuf<char> tmp;
-        BFSX_HIP_TRY(tmp.alloc(tb));
-        BFSX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tb, keys.p, keys2.p, ids.p, inv.p, (size_t)nv, 0, 32, stream));
-        BFSX_HIP_TRY(perm.alloc(nv));
-        hipLaunchKernelGGL(k_invert, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, inv.p, nv, perm.p);
+        size_t tmp_cap = 0;
+        for (int64_t r0 = 0; r0 < n; r0 += rchunk) { // one stable sort per range (ties keep id order)
+            const int64_t cnt = std::min(rchunk, n - r0);
+            hipLaunchKernelGGL(k_rank_keys, dim3(grid_for(cnt, kBS)), dim3(kBS), 0, stream, deg.p, r0, cnt, keys.p,
+                               ids.p);
+            BFSX_HIP_TRY(hipGetLastError());
+            size_t tb = 0;
+            BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys.p, keys2.p, ids.p, inv.p + r0, (size_t)cnt, 0, 32,
+                                                   stream));
+            if (tb > tmp_cap) {
+                BFSX_HIP_TRY(hipStreamSynchronize(stream));
+                tmp.reset();
+                BFSX_HIP_TRY(tmp.alloc(tb));
+                tmp_cap = tb;
+            }
+            BFSX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tb, keys.p, keys2.p, ids.p, inv.p + r0, (size_t)cnt, 0, 32,
+                                                   stream));
+        }
+        BFSX_HIP_TRY(perm.alloc(n));
+        hipLaunchKernelGGL(k_invert, dim3(grid_for(n, kBS)), dim3(kBS), 0, stream, inv.p, n, perm.p);
         BFSX_HIP_TRY(hipGetLastError());
         BFSX_HIP_TRY(hipStreamSynchronize(stream)); // temporaries are freed at the end of this scope
     }
-    // ascending rows of internal ids are degree-descending rows: no degree-order pass
-    int rc = build_rows(stream, nv, PermSrc<Src>{src, perm.p}, m, false, d_row_off_out, d_col_out, nnz_out,
-                        d_tuple_cnt_out, 0, nv_global);
+    // one device: ascending rows of internal ids are degree-descending rows, no degree-order pass
+    int rc = build_rows(stream, nv, PermSrc<Src>{src, perm.p}, m, !single, d_row_off_out, d_col_out, nnz_out,
+                        d_tuple_cnt_out, lo, nv_global);
     if (rc) return rc;
-    *d_perm_out = perm.release();
+    if (single) {
+        *d_perm_out = perm.release();
+    } else { // keep only this rank's slice of the permutation
+        DevBuf<uint32_t> loc;
+        BFSX_HIP_TRY(loc.alloc(nv));
+        if (nv > 0) {
+            hipLaunchKernelGGL(k_local_perm, dim3(grid_for(nv, kBS)), dim3(kBS), 0, stream, perm.p, lo, nv, loc.p);
+            BFSX_HIP_TRY(hipGetLastError());
+        }
+        BFSX_HIP_TRY(hipStreamSynchronize(stream));
+        *d_perm_out = loc.release();
+    }
     *d_inv_out = inv.release();
     return BFSX_OK;
 }
@@ -619,17 +654,17 @@ int export_csr_original(hipStream_t stream, int64_t nv, int64_t nnz, const int64
 }
 
 int build_csr_device(hipStream_t stream, int64_t nv, const uint32_t *d_u, const uint32_t *d_v, int64_t m,
-                     bool degree_order, bool relabel, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
+                     bool degree_order, int64_t relabel_chunk, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
                      uint32_t **d_tuple_cnt, uint32_t **d_perm, uint32_t **d_inv, int64_t lo, int64_t nv_global) {
-    return build_csr_impl(stream, nv, ArraySrc{d_u, d_v}, m, degree_order, relabel, d_row_off, d_col, nnz,
+    return build_csr_impl(stream, nv, ArraySrc{d_u, d_v}, m, degree_order, relabel_chunk, d_row_off, d_col, nnz,
                           d_tuple_cnt, d_perm, d_inv, lo, nv_global);
 }
 
-int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order, bool relabel,
-                        int64_t **d_row_off, uint32_t **d_col, int64_t *nnz, uint32_t **d_tuple_cnt, uint32_t **d_perm,
-                        uint32_t **d_inv, int64_t lo, int64_t nv_local) {
+int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t seed, bool degree_order,
+                        int64_t relabel_chunk, int64_t **d_row_off, uint32_t **d_col, int64_t *nnz,
+                        uint32_t **d_tuple_cnt, uint32_t **d_perm, uint32_t **d_inv, int64_t lo, int64_t nv_local) {
     const int64_t m = (int64_t)edgefactor << scale;
-    return build_csr_impl(stream, nv_local, KronSrc{kron_params(scale, seed)}, m, degree_order, relabel, d_row_off,
+    return build_csr_impl(stream, nv_local, KronSrc{kron_params(scale, seed)}, m, degree_order, relabel_chunk, d_row_off,
                           d_col, nnz, d_tuple_cnt, d_perm, d_inv, lo, (int64_t)1 << scale);
 }
 

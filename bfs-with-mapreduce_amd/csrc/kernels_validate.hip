@@ -96,7 +96,8 @@ int bfs_validate(bfsx_graph *g, int64_t source, const unsigned long long *stt, i
         if (!stt || g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
         if (source < 0) source = g->last_source;
     }
-    if (source < 0 || source >= (g->nranks > 1 ? g->nv_global : g->nv)) return fail(BFSX_E_ARG, "source out of range");
+    // a partition's non-owning ranks of a relabelled graph pass nv_global (the source is none of their rows)
+    if (source < 0 || source > (g->nranks > 1 ? g->nv_global : g->nv - 1)) return fail(BFSX_E_ARG, "source out of range");
     const bool part = g->nranks > 1;
     Comm *cm = g->ctx->comm.get();
     if (part && (!cm || cm->nranks != g->nranks || cm->rank != g->rank))

@@ -14,11 +14,22 @@
 //   - output: problemFile_<k> in Vertex.toString format  id|[n, ...]|[path]|distance|COLOR
 //     (Vertex.java:123-125), one line per vertex, k = number of map/reduce passes; the final file has
 //     no GRAY vertex, exactly like the reference's last file (BfsSpark.java:117)
-//   - log lines: "Application name", "Problem file", "Elapsed time [k] ==> <Stopwatch>" with Guava
-//     Stopwatch's 4-significant-digit format (BfsSpark.java:45-48,54,112)
+//   - log lines: "Application name", "Problem file", "Elapsed time [k] ==> <Stopwatch>" with Guava 18
+//     Stopwatch.toString: String.format("%.4g %s") of the integer nanoseconds in the chosen unit, Java
+//     %g rules (4 significant digits, trailing zeros kept, HALF_UP on the shortest decimal form)
+//     (BfsSpark.java:45-48,54,112)
+//   - neighbour lists in java.util.HashSet iteration order (Vertex.java:124 prints the set): the set is
+//     filled by add() in file order (GraphFileUtil.java:64-65) and re-filled in its own iteration order
+//     on every pass (Vertex.java:54-57), so every file lists a row by bucket index
+//     (h ^ h >>> 16) & (table - 1), insertion order inside a bucket, table = the smallest power of two
+//     >= 16 holding the row at load factor 0.75 (Java 8 HashMap).  Unpinned: the JVM the reference ran
+//     on (pom.xml targets 1.7; a Java 7 HashMap hashes and orders buckets differently) and bins of >= 8
+//     colliding ids in a table >= 64 (Java 8 treeifies those); the ORDER OF THE LINES of problemFile_k,
+//     k >= 1, is Spark's collectAsMap order (BfsSpark.java:110) and is written here in id order.
 // Deliberate difference: files are written with truncation (the reference opens with CREATE only and
 // leaves stale tails behind a shorter rewrite, BfsSpark.java:27,116).
 #include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <cinttypes>
 #include <cmath>
@@ -48,22 +59,62 @@ void log_line(const char *level, const char *method, int line, const std::string
     std::fflush(stdout);
 }
 
-// Guava Stopwatch.toString: 4 significant digits, unit chosen by magnitude (ns, μs, ms, s, min, h, d).
-std::string stopwatch_string(double nanos) {
-    static const struct {
-        double scale;
-        const char *abbr;
-    } units[] = {{86400e9, "d"}, {3600e9, "h"}, {60e9, "min"}, {1e9, "s"}, {1e6, "ms"}, {1e3, "μs"}, {1, "ns"}};
-    for (const auto &u : units) {
-        if (nanos >= u.scale || u.scale == 1) {
-            char buf[64];
-            const double v = nanos / u.scale;
-            // %.4g, like Platform.formatCompact4Digits
-            std::snprintf(buf, sizeof(buf), "%.4g %s", v, u.abbr);
-            return buf;
+// Java's String.format("%.4g", v) for v >= 0 (java.util.Formatter GENERAL conversion): the shortest
+// decimal form of v (Double.toString's digits) rounded HALF_UP to 4 significant digits; plain notation
+// when the rounded value is in [1e-4, 1e4), else d.ddde+XX; trailing zeros kept (1.5 -> "1.500").
+std::string java_format_4g(double v) {
+    if (!(v > 0.0)) return "0.000";
+    char buf[64];
+    const auto r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific); // shortest
+    const std::string sci(buf, r.ptr);
+    const size_t epos = sci.find('e');
+    std::string dig;
+    for (size_t i = 0; i < epos; i++)
+        if (sci[i] != '.') dig += sci[i];
+    int exp10 = std::atoi(sci.c_str() + epos + 1); // v = d.ddd * 10^exp10
+    if (dig.size() > 4) {
+        const bool up = dig[4] >= '5';
+        dig.resize(4);
+        if (up) {
+            int i = 3;
+            while (i >= 0 && dig[i] == '9') dig[i--] = '0';
+            if (i >= 0) {
+                dig[i]++;
+            } else { // 9999.5 -> 1000e+1
+                dig = "1000";
+                exp10++;
+            }
         }
     }
-    return "0 ns";
+    while (dig.size() < 4) dig += '0';
+    std::string out;
+    if (exp10 >= -4 && exp10 < 4) {
+        if (exp10 >= 0) {
+            out = dig.substr(0, exp10 + 1);
+            if (exp10 < 3) out += "." + dig.substr(exp10 + 1);
+        } else {
+            out = "0." + std::string(-exp10 - 1, '0') + dig;
+        }
+    } else {
+        char e[16];
+        std::snprintf(e, sizeof(e), "e%c%02d", exp10 < 0 ? '-' : '+', exp10 < 0 ? -exp10 : exp10);
+        out = dig.substr(0, 1) + "." + dig.substr(1) + e;
+    }
+    return out;
+}
+
+// Guava 18 Stopwatch.toString (Stopwatch.java: chooseUnit + String.format("%.4g %s")): the elapsed
+// integer nanoseconds in the largest unit they reach (d, h, min, s, ms, μs, ns).
+std::string stopwatch_string(int64_t nanos) {
+    static const struct {
+        int64_t scale;
+        const char *abbr;
+    } units[] = {{86400000000000LL, "d"}, {3600000000000LL, "h"}, {60000000000LL, "min"}, {1000000000LL, "s"},
+                 {1000000LL, "ms"},       {1000LL, "μs"},       {1LL, "ns"}};
+    for (const auto &u : units)
+        if (nanos / u.scale > 0 || u.scale == 1)
+            return java_format_4g((double)nanos / (double)u.scale) + " " + u.abbr;
+    return "0.000 ns";
 }
 
 // ---- java.util.Properties (subset: comments, '=' / ':' / whitespace separators, continuation lines,
@@ -134,6 +185,66 @@ std::vector<std::string> split_commas(const std::string &s) { // Splitter.on(","
 
 bool truthy(const std::string &v) { return v == "true" || v == "TRUE" || v == "True" || v == "1"; }
 
+// ---- neighbour rows in java.util.HashSet iteration order (see the header) ----------------------------
+// Rows are filled in file order (GraphFileUtil.java:64-65: vertex1 gets vertex2, then vertex2 gets
+// vertex1; a repeated neighbour or a self-loop's second add changes nothing), then each row is stably
+// ordered by its Java 8 HashMap bucket.  Out: off/col of the rows in output order.
+int hashset_rows(const std::string &file, int64_t nv, std::vector<int64_t> &off, std::vector<uint32_t> &col) {
+    int64_t pnv = 0, m = 0;
+    uint32_t *u = nullptr, *v = nullptr;
+    if (int rc = bfsx_parse_algs4(file.c_str(), &pnv, &m, &u, &v)) return rc;
+    if (pnv != nv) {
+        bfsx_free_host(u);
+        bfsx_free_host(v);
+        return BFSX_E_PARSE;
+    }
+    std::vector<int64_t> cnt(nv + 1, 0);
+    for (int64_t i = 0; i < m; i++) {
+        cnt[u[i] + 1]++;
+        cnt[v[i] + 1]++;
+    }
+    for (int64_t x = 0; x < nv; x++) cnt[x + 1] += cnt[x];
+    std::vector<uint32_t> raw(cnt[nv]);
+    std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
+    for (int64_t i = 0; i < m; i++) { // insertion order of every row
+        raw[cur[u[i]]++] = v[i];
+        raw[cur[v[i]]++] = u[i];
+    }
+    bfsx_free_host(u);
+    bfsx_free_host(v);
+    off.assign(nv + 1, 0);
+    col.clear();
+    col.reserve(raw.size());
+    std::vector<uint32_t> row;
+    std::vector<std::pair<uint32_t, uint32_t>> keyed; // (bucket, insertion rank)
+    for (int64_t x = 0; x < nv; x++) {
+        row.assign(raw.begin() + cnt[x], raw.begin() + cnt[x + 1]);
+        // first occurrences, in order
+        std::vector<std::pair<uint32_t, uint32_t>> firsts;
+        firsts.reserve(row.size());
+        for (uint32_t i = 0; i < row.size(); i++) firsts.push_back({row[i], i});
+        std::stable_sort(firsts.begin(), firsts.end(),
+                         [](const std::pair<uint32_t, uint32_t> &a, const std::pair<uint32_t, uint32_t> &b) {
+                             return a.first < b.first;
+                         });
+        std::vector<std::pair<uint32_t, uint32_t>> uniq; // (insertion rank, id)
+        for (size_t i = 0; i < firsts.size(); i++)
+            if (i == 0 || firsts[i].first != firsts[i - 1].first) uniq.push_back({firsts[i].second, firsts[i].first});
+        std::sort(uniq.begin(), uniq.end());
+        uint64_t table = 16;
+        while (uniq.size() > table * 3 / 4) table *= 2; // resize when size > 0.75 * capacity
+        keyed.clear();
+        for (uint32_t i = 0; i < uniq.size(); i++) {
+            const uint32_t h = uniq[i].second;
+            keyed.push_back({(uint32_t)((h ^ (h >> 16)) & (table - 1)), i});
+        }
+        std::stable_sort(keyed.begin(), keyed.end()); // ties: insertion rank ascending
+        for (const auto &k : keyed) col.push_back(uniq[k.second].second);
+        off[x + 1] = (int64_t)col.size();
+    }
+    return BFSX_OK;
+}
+
 // ---- Vertex.toString writer (Vertex.java:123-125) -------------------------------------------------
 // state after map/reduce pass `k` (k = levels: final state).  A vertex at distance d < k is BLACK,
 // d == k is GRAY (discovered by pass k), d > k or unreachable is WHITE with Integer.MAX_VALUE and the
@@ -147,8 +258,7 @@ bool write_state(const std::string &file, int64_t nv, const std::vector<int64_t>
     std::string buf;
     buf.reserve(1 << 20);
     for (int64_t v = 0; v < nv; v++) {
-        row.assign(col.begin() + off[v], col.begin() + off[v + 1]);
-        std::sort(row.begin(), row.end());
+        row.assign(col.begin() + off[v], col.begin() + off[v + 1]); // already in HashSet order
         const int32_t d = dist[v];
         const bool reached = d != INT32_MAX && d <= k;
         buf += std::to_string(v);
@@ -197,7 +307,13 @@ int run_problem(bfsx_ctx *ctx, const std::string &problem, int64_t source, bool 
     std::vector<uint32_t> col(std::max<int64_t>(nnz, 1));
     std::vector<int32_t> dist(nv, INT32_MAX);
     std::vector<int64_t> parent(nv, -1);
-    if ((rc = bfsx_graph_csr(g, off.data(), col.data()))) goto out;
+    // the rows as the reference prints them (the device CSR holds the same sets, degree-ordered)
+    if ((rc = hashset_rows(problem, nv, off, col))) goto out;
+    if ((int64_t)col.size() != nnz) {
+        log_line("ERROR", "main", 55, "adjacency of the written rows differs from the device graph");
+        rc = BFSX_E_PARSE;
+        goto out;
+    }
     if (source < 0 || source >= nv) {
         log_line("ERROR", "main", 55, "source vertex outside the graph");
         rc = BFSX_E_RANGE;
@@ -221,7 +337,7 @@ int run_problem(bfsx_ctx *ctx, const std::string &problem, int64_t source, bool 
         bfsx_level_times(g, cum.data(), st.levels);
         for (int k = 1; k <= st.levels; k++) {
             log_line("INFO", "main", 112, "Elapsed time [" + std::to_string(k) + "] ==> " +
-                                              stopwatch_string(cum[k - 1] * 1e6));
+                                              stopwatch_string(std::llround(cum[k - 1] * 1e6)));
             const bool last = k == st.levels;
             if ((dump_levels || last) &&
                 !write_state(problem + "_" + std::to_string(k), nv, off, col, dist, parent, source, k, paths)) {
@@ -260,8 +376,11 @@ int main(int argc, char **argv) {
     std::string props_path = "service.properties"; // ServiceConfiguration.CONFIGURATION_FILE (:18)
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "--properties") && i + 1 < argc) props_path = argv[++i];
-        else if (!std::strcmp(argv[i], "--help")) {
-            std::printf("usage: bfsx_spark [--properties service.properties]\n");
+        else if (!std::strcmp(argv[i], "--format-nanos")) { // the Stopwatch format of each argument (tests)
+            for (int j = i + 1; j < argc; j++) std::printf("%s\n", stopwatch_string(std::strtoll(argv[j], nullptr, 10)).c_str());
+            return 0;
+        } else if (!std::strcmp(argv[i], "--help")) {
+            std::printf("usage: bfsx_spark [--properties service.properties] | --format-nanos N...\n");
             return 0;
         }
     }

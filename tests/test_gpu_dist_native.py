@@ -91,13 +91,17 @@ def test_native_group_random(bfsx, world, direction):
     check(nv, u, v, sources, out)
 
 
+@pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_native_group_kronecker(bfsx, world):
+def test_native_group_kronecker(bfsx, world, relabel):
+    """relabel on (the default): every rank's id range renumbered by degree inside the range (ownership
+    unchanged); the results come back in original ids either way."""
     scale, seed = 16, 0xD157
     u, v = O.kronecker(scale, 16, seed)
     nv = 1 << scale
     sources = [int(u[0]), int(u[777])]
-    out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, seed=seed), sources)
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, seed=seed), sources,
+                    options={"relabel": relabel})
     check(nv, u, v, sources, out)
     assert any(2 in o[3] for o in out)  # a bottom-up level ran against the all-gathered frontier
     # the partitioned result equals the single-device result bit for bit
@@ -105,6 +109,53 @@ def test_native_group_kronecker(bfsx, world):
         for s, o in zip(sources, out):
             d, _, _ = g.bfs(s)
             assert np.array_equal(d, o[1])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_group_relabel_ranges(bfsx, world):
+    """A relabelled partition keeps every id in its owner's range: each rank's CSR (exported in original
+    ids) holds exactly its original rows, and the collective validator accepts the result for a source
+    given explicitly on every rank (only its owner knows the source's internal id)."""
+    rng = np.random.default_rng(7 + world)
+    nv = 5000
+    u = rng.integers(0, nv, 6 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 6 * nv).astype(np.uint32)
+    off, col = O.build_sets(nv, u, v)
+    ctxs = [bfsx.Context(0) for _ in range(world)]
+    graphs = [None] * world
+    try:
+        bfsx.local_group(ctxs)
+        for r in range(world):
+            graphs[r] = ctxs[r].dist_from_edges(nv, u, v, r, world)
+        for r in range(world):
+            p = graphs[r].partition()
+            lo, n = p["v_lo"], p["nv_local"]
+            goff, gcol = graphs[r].csr()
+            for x in range(0, n, 97):
+                assert set(gcol[goff[x]:goff[x + 1]].tolist()) == set(col[off[lo + x]:off[lo + x + 1]].tolist())
+            assert goff[n] == off[lo + n] - off[lo]
+        res, errs = [None] * world, []
+
+        def work(r):
+            try:
+                graphs[r].dist_bfs(1234)
+                res[r] = graphs[r].validate(1234)
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errs.append(repr(e))
+
+        ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=120)
+        assert not errs, errs
+        assert all(x["errors"] == 0 for x in res) and res[0]["reached"] > 0
+    finally:
+        for g in graphs:
+            if g is not None:
+                g.free()
+        for c in ctxs:
+            c.close()
 
 
 def test_native_group_int64_offsets(bfsx):

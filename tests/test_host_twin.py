@@ -38,6 +38,56 @@ def write_props(d, files, extra=""):
                 f"problemFiles={','.join(files)}\n{extra}")
 
 
+def java_4g(x):
+    """String.format("%.4g", x) (java.util.Formatter GENERAL): HALF_UP on the shortest decimal digits."""
+    from decimal import ROUND_HALF_UP, Decimal
+    if x == 0:
+        return "0.000"
+    d = Decimal(repr(x))
+    e = d.adjusted()
+    q = d.quantize(Decimal(1).scaleb(e - 3), rounding=ROUND_HALF_UP)
+    if q.adjusted() != e:  # 9999.5 -> 1.000e4
+        e = q.adjusted()
+        q = d.quantize(Decimal(1).scaleb(e - 3), rounding=ROUND_HALF_UP)
+    if -4 <= e < 4:
+        return f"{q:.{max(3 - e, 0)}f}"
+    m = q.scaleb(-e)
+    return f"{m:.3f}e{'+' if e >= 0 else '-'}{abs(e):02d}"
+
+
+def guava_stopwatch(nanos):
+    """Guava 18 Stopwatch.toString (BfsSpark.java:112): largest unit reached, then %.4g."""
+    for scale, abbr in ((86400 * 10**9, "d"), (3600 * 10**9, "h"), (60 * 10**9, "min"), (10**9, "s"),
+                        (10**6, "ms"), (10**3, "\u03bcs"), (1, "ns")):
+        if nanos // scale > 0 or scale == 1:
+            return java_4g(nanos / scale) + " " + abbr
+
+
+def test_stopwatch_format():
+    """The twin's "Elapsed time [k] ==> ..." value: Java keeps trailing zeros (1.5 ms -> "1.500 ms")."""
+    vals = [0, 1, 7, 999, 1000, 1500, 99999, 123456, 999949, 999950, 1500000, 12345678901, 59999999999,
+            3599999999999, 86400000000000, 864000000000000000]
+    r = subprocess.run([BIN, "--format-nanos"] + [str(x) for x in vals], capture_output=True, text=True)
+    assert r.returncode == 0
+    got = r.stdout.strip().split("\n")
+    assert got == [guava_stopwatch(x) for x in vals]
+    assert got[:3] == ["0.000 ns", "1.000 ns", "7.000 ns"] and "1.500 ms" in got and "1000 \u03bcs" in got
+
+
+def java_hashset_order(ids):
+    """Iteration order of a java.util.HashSet<Integer> filled by add() in this order (Java 8 HashMap:
+    bucket (h ^ h >>> 16) & (table - 1), insertion order inside a bucket, table >= 16 at load 0.75)."""
+    seen, uniq = set(), []
+    for x in ids:
+        if x not in seen:
+            seen.add(x)
+            uniq.append(x)
+    table = 16
+    while len(uniq) > table * 3 // 4:
+        table *= 2
+    return sorted(uniq, key=lambda h: (h ^ (h >> 16)) & (table - 1))  # sorted() is stable
+
+
 def test_missing_properties_fails(tmp_path):
     r = subprocess.run([BIN], cwd=tmp_path, capture_output=True, text=True)
     assert r.returncode == 2
@@ -93,6 +143,18 @@ def test_bfs_spark_twin_end_to_end(tmp_path):
         assert not os.path.exists(tmp_path / f"{n}.txt_{passes[n] + 1}")
         final = read_state(tmp_path / f"{n}.txt_{passes[n]}")
         assert not any(t[4] == "GRAY" for t in final.values())  # termination (BfsSpark.java:117)
+    # neighbour lists printed in HashSet iteration order (Vertex.java:124), rows filled in file order
+    nv, u, v = O.load_graphfileutil(str(tmp_path / "mediumG.txt"))
+    rows = [[] for _ in range(nv)]
+    for a, b in zip(u.tolist(), v.tolist()):
+        rows[a].append(b)
+        rows[b].append(a)
+    for k in (0, passes["mediumG"]):
+        with open(tmp_path / f"mediumG.txt_{k}") as f:
+            for line in f.read().split("\n"):
+                vid, lst = line.split("|")[0], line.split("|")[1]
+                got = [int(x) for x in lst.strip("[]").split(", ") if x]
+                assert got == java_hashset_order(rows[int(vid)]), vid
     # "Elapsed time [k]" for every pass, like BfsSpark.java:112
     for k in range(1, 15):
         assert f"Elapsed time [{k}] ==> " in r.stdout
