@@ -427,13 +427,16 @@ def run_dist(args, world, rank, local_rank):
     ctx.synchronize()
     dist.barrier()
     w0 = time.perf_counter()
-    dev_ms, order = [], []
+    dev_ms, order, all_levels = [], [], []
     for _ in range(args.steps):
         for r in roots:
             dev_ms.append(g.dist_bfs(r, want_stats=False))
             order.append(r)
             if rank == 0:
-                acct.add(g.level_stats(256))
+                lv = g.level_stats(256)
+                acct.add(lv)
+                if args.levels_json:
+                    all_levels.extend(dict(ls, root=r) for ls in lv)
     ctx.synchronize()
     wall_local = time.perf_counter() - w0
     dist.barrier()
@@ -460,6 +463,9 @@ def run_dist(args, world, rank, local_rank):
                                    "rules": "Graph500 kernel-2 + BreadthFirstPaths.check, on device, collective"},
                     "levels_last": [{k: ls[k] for k in ("level", "direction", "frontier_in", "frontier_out",
                                                         "kernel_ms")} for ls in g.level_stats(256)]})
+    if rank == 0 and args.levels_json:
+        with open(args.levels_json, "w") as f:
+            json.dump(all_levels, f)
     g.free()
     ctx.close()
     dist.destroy_process_group()

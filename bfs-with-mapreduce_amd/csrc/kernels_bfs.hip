@@ -292,14 +292,20 @@ __device__ inline void publish_if_last(LevelSlot *slot, Published *pub, u64 seq)
 // serialises at the memory side (measured 2.4 G edges/s on scale 26 with per-wave appends).
 constexpr int kQCap = 4096;
 
-struct BlockQueue {
-    uint32_t buf[kQCap];
+template <int kCapT>
+struct BlockQueueT {
+    static constexpr uint32_t kCap = kCapT;
+    uint32_t buf[kCapT];
     uint32_t n;
     uint32_t gbase;
 };
+using BlockQueue = BlockQueueT<kQCap>;
+// the partitioned push kernels also hold a remote-pair queue: half-size queues keep 4 workgroups per CU
+using DistQueue = BlockQueueT<kQCap / 2>;
 
 // All 64 lanes of every wave call this (wave-uniform control flow).
-__device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
+template <class Q>
+__device__ inline void bq_push(Q &q, bool win, uint32_t v) {
     const u64 mask = __ballot(win);
     if (mask == 0) return;
     const unsigned lane = lane_id();
@@ -311,7 +317,8 @@ __device__ inline void bq_push(BlockQueue &q, bool win, uint32_t v) {
 }
 
 // Block-uniform: every thread calls after a __syncthreads().
-__device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, u64 *qtail) {
+template <class Q>
+__device__ inline void bq_flush(Q &q, uint32_t *__restrict__ qout, u64 *qtail) {
     const uint32_t n = q.n;
     if (n == 0) return;
     if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(qtail, (u64)n);
@@ -323,7 +330,8 @@ __device__ inline void bq_flush(BlockQueue &q, uint32_t *__restrict__ qout, u64 
     __syncthreads();
 }
 
-__device__ inline void bq_init(BlockQueue &q) {
+template <class Q>
+__device__ inline void bq_init(Q &q) {
     if (threadIdx.x == 0) q.n = 0;
 }
 
@@ -368,7 +376,7 @@ struct Part {
 };
 
 // Remote pairs, LDS-buffered like the local queue (multi-GPU path only).
-constexpr int kRCap = 2048;
+constexpr int kRCap = 1024;
 struct RemoteQueue {
     u64 buf[kRCap];
     u64 gbase; // 64-bit: a forced top-down level at scale 30 can route more than 2^32 pairs
@@ -400,11 +408,11 @@ __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
 
 // Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries; u = local row id)
 // in steps of kBS*kItems.  Block-uniform.  kDist: targets owned by another rank become remote pairs.
-template <bool kDist, class OffT, class ScanT>
+template <bool kDist, class OffT, class ScanT, class Q>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                      int32_t nd, BlockQueue &q, uint32_t *__restrict__ qout, u64 *qtail,
+                                      int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
                                       HubSet hs, u64 &acc_mfh, u64 &acc_nh) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
@@ -450,7 +458,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
             if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
         }
         __syncthreads();
-        if (q.n > (uint32_t)(kQCap - kBS * kItems)) bq_flush(q, qout, qtail);
+        if (q.n > Q::kCap - (uint32_t)(kBS * kItems)) bq_flush(q, qout, qtail);
         if (kDist && rq->n > (uint32_t)(kRCap - kBS * kItems)) rq_flush(*rq, pt);
     }
 }
@@ -468,7 +476,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     __shared__ int64_t s_beg[kBS];
     __shared__ uint32_t s_u[kBS];
     __shared__ uint32_t s_wsum[kWaves];
-    __shared__ BlockQueue q;
+    __shared__ typename std::conditional<kDist, DistQueue, BlockQueue>::type q;
     __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
@@ -538,7 +546,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     __shared__ int64_t s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
     __shared__ u64 s_tsum[kBS];
-    __shared__ BlockQueue q;
+    __shared__ typename std::conditional<kDist, DistQueue, BlockQueue>::type q;
     __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
@@ -1110,7 +1118,7 @@ __device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *_
 // overlap the probes, stage A2 and phase B instead of opening the next round (one dependent memory
 // latency fewer per round; a half-group of dense candidates runs up to 8 rounds).
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 6 : (kU == 4 ? 5 : 6)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 6 : (kU == 4 ? ((kMf && kPipe) ? 4 : 5) : 6)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
@@ -1583,8 +1591,11 @@ __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict_
 
 // Multi-GPU level close: one workgroup sums the level's counter shards into
 //   out[0..6] = local {n_f, m_f, m_u, scanned, rows/claims, stage2, walked}   out[8..10] = copy of {n_f, m_f, m_u}
-// (the copy is all-reduced in place; the local half stays for the per-level record).
-__global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out) {
+// (the copy is all-reduced in place; the local half stays for the per-level record), and zeroes the
+// next top-down level's exchange counters `ctr` (nothing reads them after this level's claim kernel).
+__global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
+                             u64 *__restrict__ ctr, int nctr) {
+    for (int i = threadIdx.x; i < nctr; i += blockDim.x) ctr[i] = 0ull;
     __shared__ u64 s[kStatFields][kShards];
     for (int i = threadIdx.x; i < kShards; i += blockDim.x) {
         s[0][i] = slot->sh[i].nf;
@@ -1875,10 +1886,10 @@ template <class OffT, bool kMf, bool kHubs>
 int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
                 u64 seq) {
     if (g->ctx->opt.bu_unroll == 2) return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, level, pub, seq);
-    // kMf (partitioned) + kPipe needs more than the 96 VGPRs of 5 waves per SIMD: it would spill, so the
-    // partitioned pull level runs unpipelined
-    return g->ctx->opt.bu_pipeline && !kMf
-               ? launch_bu_u<OffT, kMf, kHubs, 4, false, !kMf>(g, ws, row_off, front, level, pub, seq)
+    // kMf (partitioned) + kPipe needs more than the 96 VGPRs of 5 waves per SIMD: that instantiation runs
+    // at 4 waves per SIMD (a spilling pull kernel is never an option)
+    return g->ctx->opt.bu_pipeline
+               ? launch_bu_u<OffT, kMf, kHubs, 4, false, true>(g, ws, row_off, front, level, pub, seq)
                : launch_bu_u<OffT, kMf, kHubs, 4, false, false>(g, ws, row_off, front, level, pub, seq);
 }
 
@@ -2709,7 +2720,8 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) 
     hipStream_t st = g->ctx->stream;
     const int level = ws->d_level;
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
-    hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums);
+    hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums,
+                       ws->d_dist_ctr, kCtrHead);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3, st)) return e;
@@ -2767,11 +2779,19 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
     const int64_t deg = ws->h_gdeg[source]; // original ids index the padded slices directly (v_lo = rank * chunk)
     int64_t deg_local = 0;
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st)); // before the timed region
     if ((rc = dist_begin(g, source, &deg_local, deg))) return rc;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
+    const bool owner = source >= g->v_lo && source < g->v_lo + g->nv;
     int64_t nf = 1, prev_nf = 0, mf = deg, mu = ws->nnz_global - deg, examined = 0;
-    int64_t visited_local = (source >= g->v_lo && source < g->v_lo + g->nv) ? 1 : 0;
+    // m_u of this rank's unvisited rows.  A pull level reports the exact m_u it leaves (the degree sum
+    // of its unvisited candidates), so the m_f of the frontier it found is the m_u it consumed: no
+    // per-discovery degree read in the pull kernel.  Before the first pull level the count still holds
+    // the isolated self-loop-only rows' entries, which can only over-state that m_f (a safe bound for
+    // the next push level's pair buffers).
+    int64_t mu_local = g->nnz - (owner ? deg : 0);
+    int64_t visited_local = owner ? 1 : 0;
     bool snapped = false; // ws->front holds the visited slice from before the last (top-down) level
     int td_levels = 0, bu_levels = 0;
     ExchangePlan plan;
@@ -2820,14 +2840,15 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
             }
             if (int e = grow(ws->sendbuf, ws->send_cap, need)) return e;
-            BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st));
+            // the exchange counters are zero: dist_bfs_run zeroes them before the first level, every
+            // level's k_level_sums after its exchange
             const Part pt = make_part(g, ws);
             if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, -1, level, pt)) return e;
             u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
             const unsigned gbk = clamp_grid((need + kBS - 1) / kBS, 1024);
             int64_t slot = 0, ro = 0; // slot > 0: fixed-slot exchange
-            if (P > 1 && mf <= opt.slot_pairs) {
+            if (mf <= opt.slot_pairs) {
                 // small level: no rank sends more than the global m_f pairs to any peer, so every peer gets
                 // a fixed slot [count, m_f pairs] -- one exchange, no count all-to-all, no host wait
                 slot = std::max<int64_t>(mf, 1);
@@ -2885,7 +2906,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 ws->d_in_queue = false;
             }
             if (int e = cm->allgather(ws->front, ws->nwords, ws->fglob, st)) return e;
-            if (int e = launch_bu<true>(g, ws, ws->fglob, level)) return e;
+            if (int e = launch_bu<false>(g, ws, ws->fglob, level)) return e; // m_f from m_u (below)
             bu_levels++;
         }
         if (int e = dist_level_close(g, ws, td, h)) return e;
@@ -2910,12 +2931,20 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         ws->d_dir = dir;
         ws->d_in_queue = td;
         ws->d_nf = h[0];
-        ws->d_mf = h[1];
         ws->d_level = level + 1;
         prev_nf = nf;
         nf = h[8];
-        mf = h[9];
-        mu = td ? mu - mf : h[10];
+        if (td) { // the push kernels and the claims sum the degrees of what they discover
+            ws->d_mf = h[1];
+            mf = h[9];
+            mu -= mf;
+            mu_local -= h[1];
+        } else { // the pull kernel reports the m_u it leaves: what it found held the difference
+            ws->d_mf = std::max<int64_t>(mu_local - h[2], 0);
+            mf = std::max<int64_t>(mu - h[10], 0);
+            mu = h[10];
+            mu_local = h[2];
+        }
         if (nf == 0) break;
     }
     if ((rc = dist_finish(g))) return rc;
