@@ -17,11 +17,11 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC
 
 all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark oracle
 
-$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/bfsx_internal.h include/bfsx.h
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h include/bfsx.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h include/bfsx.h
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h include/bfsx.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -16,6 +16,7 @@
 #include <unordered_set>
 
 #include "bfsx_internal.h"
+#include "java_digits.h"
 
 namespace bfsx {
 
@@ -37,27 +38,9 @@ inline uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// Integer.parseInt over an exact token: optional sign, >= 1 ASCII digit, int32 range, no trimming.
+// Integer.parseInt over the exact token, no trimming (Unicode decimal digits included, java_digits.h)
 inline bool parse_java_int(const char *s, size_t n, int64_t &out) {
-    if (n == 0) return false;
-    size_t i = 0;
-    bool neg = false;
-    if (s[0] == '+' || s[0] == '-') {
-        neg = s[0] == '-';
-        if (n == 1) return false;
-        i = 1;
-    }
-    int64_t val = 0;
-    for (; i < n; i++) {
-        const unsigned d = (unsigned)(s[i] - '0');
-        if (d > 9) return false;
-        val = val * 10 + d;
-        if (val > 2147483648LL) return false;
-    }
-    if (neg) val = -val;
-    if (val > 2147483647LL) return false;
-    out = val;
-    return true;
+    return java_parse_int(reinterpret_cast<const unsigned char *>(s), 0, (int64_t)n, out);
 }
 
 struct MappedFile {

@@ -9,6 +9,7 @@
 //   2. one thread per line parses its two tokens, writing the tuple in place (u[line], v[line]);
 //   3. the first bad line in file order (an atomicMin over (line, code)) reproduces the host parser's
 //      error -- the same code (E_PARSE before E_RANGE within a line) and the same line number.
+// Tokens follow Integer.parseInt, Unicode decimal digits included (java_digits.h).
 // The tuples stay on the device for the CSR build: a 7.6 M-edge file is ~100 MB of text but 61 MB of
 // tuples that no longer cross PCIe.
 #include <rocprim/device/device_select.hpp>
@@ -16,6 +17,7 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include "bfsx_internal.h"
+#include "java_digits.h"
 
 namespace bfsx {
 
@@ -31,27 +33,6 @@ struct LineStart {
         return (p == '\n' || (p == '\r' && b[i] != '\n')) ? 1 : 0;
     }
 };
-
-// Integer.parseInt over the exact token [s, e): optional sign, >= 1 ASCII digit, int32 range.
-__device__ inline bool java_int(const char *b, int64_t s, int64_t e, int64_t &out) {
-    if (s >= e) return false;
-    bool neg = false;
-    if (b[s] == '+' || b[s] == '-') {
-        neg = b[s] == '-';
-        if (++s == e) return false;
-    }
-    int64_t val = 0;
-    for (; s < e; s++) {
-        const unsigned d = (unsigned)(b[s] - '0');
-        if (d > 9) return false;
-        val = val * 10 + d;
-        if (val > 2147483648LL) return false;
-    }
-    if (neg) val = -val;
-    if (val > 2147483647LL) return false;
-    out = val;
-    return true;
-}
 
 constexpr unsigned long long kErrParse = 1, kErrRange = 2;
 
@@ -72,7 +53,8 @@ __global__ __launch_bounds__(kBS) void k_parse_lines(const char *__restrict__ b,
         } else {
             int64_t sp2 = sp + 1;
             while (sp2 < e && b[sp2] != ' ') sp2++;
-            if (!java_int(b, s, sp, a) || !java_int(b, sp + 1, sp2, c)) code = kErrParse;
+            const unsigned char *ub = reinterpret_cast<const unsigned char *>(b);
+            if (!java_parse_int(ub, s, sp, a) || !java_parse_int(ub, sp + 1, sp2, c)) code = kErrParse;
             else if (a < 0 || a >= nv || c < 0 || c >= nv) code = kErrRange;
         }
         if (code) {

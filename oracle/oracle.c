@@ -50,22 +50,76 @@ static int next_line(const char *buf, size_t len, size_t *pos, const char **ls, 
     return 1;
 }
 
-/* java.lang.Integer.parseInt over an exact token (no trimming): [+-]?[0-9]+ within int32. */
+/* InputStreamReader (UTF-8, the Linux platform charset; GraphFileUtil.java:46) turns the token's bytes
+ * into UTF-16 chars: a malformed sequence becomes U+FFFD, a 4-byte sequence a surrogate pair.  Writes
+ * at most n chars to w and returns their count. */
+static size_t utf8_to_utf16(const unsigned char *s, size_t n, uint32_t *w) {
+    size_t i = 0, k = 0;
+    while (i < n) {
+        const unsigned c = s[i];
+        int len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+        uint32_t cp = len == 1 ? c : len == 2 ? (c & 31u) : len == 3 ? (c & 15u) : (c & 7u);
+        int ok = len > 0 && i + (size_t)len <= n;
+        for (int j = 1; ok && j < len; j++) {
+            if ((s[i + j] & 0xC0u) != 0x80u) ok = 0;
+            else cp = (cp << 6) | (s[i + j] & 0x3Fu);
+        }
+        if (ok && ((len == 2 && cp < 0x80) || (len == 3 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) ||
+                   (len == 4 && (cp < 0x10000 || cp > 0x10FFFF))))
+            ok = 0;
+        if (!ok) {
+            w[k++] = 0xFFFD;
+            i++;
+            continue;
+        }
+        if (cp >= 0x10000) {
+            w[k++] = 0xD800 + ((cp - 0x10000) >> 10);
+            w[k++] = 0xDC00 + ((cp - 0x10000) & 0x3FF);
+        } else {
+            w[k++] = cp;
+        }
+        i += (size_t)len;
+    }
+    return k;
+}
+
+/* Character.digit(ch, 10) on a UTF-16 char: the Unicode Nd digits of the BMP that Java 8 (Unicode 6.2)
+ * knows, one entry per block of ten (Character.getType(ch) == DECIMAL_DIGIT_NUMBER). */
+static int java_char_digit(uint32_t ch) {
+    static const uint32_t zero[] = {0x0030, 0x0660, 0x06F0, 0x07C0, 0x0966, 0x09E6, 0x0A66, 0x0AE6, 0x0B66,
+                                    0x0BE6, 0x0C66, 0x0CE6, 0x0D66, 0x0E50, 0x0ED0, 0x0F20, 0x1040, 0x1090,
+                                    0x17E0, 0x1810, 0x1946, 0x19D0, 0x1A80, 0x1A90, 0x1B50, 0x1BB0, 0x1C40,
+                                    0x1C50, 0xA620, 0xA8D0, 0xA900, 0xA9D0, 0xAA50, 0xABF0, 0xFF10};
+    for (size_t i = 0; i < sizeof(zero) / sizeof(zero[0]); i++)
+        if (ch >= zero[i] && ch <= zero[i] + 9) return (int)(ch - zero[i]);
+    return -1;
+}
+
+/* java.lang.Integer.parseInt over an exact token (no trimming): an optional '+'/'-', then chars that
+ * Character.digit maps to 0..9, within int32. */
 static int java_parse_int(const char *s, size_t n, int64_t *out) {
     if (n == 0) return ORC_E_PARSE;
+    uint32_t stackbuf[64];
+    uint32_t *w = n <= 64 ? stackbuf : (uint32_t *)malloc(n * sizeof(uint32_t));
+    if (!w) return ORC_E_OOM;
+    const size_t k = utf8_to_utf16((const unsigned char *)s, n, w);
+    int rc = ORC_OK;
     size_t i = 0;
     int neg = 0;
-    if (s[0] == '-' || s[0] == '+') {
-        neg = s[0] == '-';
+    if (w[0] == '-' || w[0] == '+') {
+        neg = w[0] == '-';
         i = 1;
-        if (n == 1) return ORC_E_PARSE;
+        if (k == 1) rc = ORC_E_PARSE;
     }
     int64_t val = 0;
-    for (; i < n; i++) {
-        if (s[i] < '0' || s[i] > '9') return ORC_E_PARSE;
-        val = val * 10 + (s[i] - '0');
-        if (val > 2147483648LL) return ORC_E_PARSE;
+    for (; rc == ORC_OK && i < k; i++) {
+        const int d = java_char_digit(w[i]);
+        if (d < 0) rc = ORC_E_PARSE;
+        val = val * 10 + d;
+        if (val > 2147483648LL) rc = ORC_E_PARSE;
     }
+    if (w != stackbuf) free(w);
+    if (rc) return rc;
     if (neg) val = -val;
     if (val > 2147483647LL || val < -2147483648LL) return ORC_E_PARSE;
     *out = val;

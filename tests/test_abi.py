@@ -68,14 +68,32 @@ MALFORMED = {
     "overflow": "3\n1\n0 2147483648\n",
     "tab_sep": "3\n1\n0\t1\n",
     "ok_trailing_space": "3\n1\n0 1 \n",  # ["0","1",""]: get(0), get(1) parse fine
+    # Integer.parseInt takes every BMP char Character.digit maps to 0..9 (Unicode Nd), after the
+    # InputStreamReader's UTF-8 decoding (GraphFileUtil.java:46,48,62-63)
+    "ok_arabic_indic": "\u0663\n\u0662\n\u0660 \u0661\n\u0661 \u0662\n",
+    "ok_fullwidth": "\uff13\n1\n\uff10 \uff12\n",
+    "ok_mixed_scripts": "20\n1\n1\u0967 \u0660\n",  # "1" + Devanagari one = 11
+    "ok_plus_unicode": "3\n1\n+\u0662 0\n",
+    "range_unicode": "3\n1\n\u0663 0\n",
+    "bad_supplementary_digit": "3\n1\n\U0001D7CE 1\n",  # two surrogate chars: not digits
+    "bad_unicode7_digit": "3\n1\n\u0de6 1\n",  # Sinhala Lith zero: Unicode 7.0, after Java 8's tables
+    "bad_superscript": "3\n1\n\u00b2 1\n",  # category No, not Nd
+    "bad_invalid_utf8": b"3\n1\n0\xff 1\n",  # decodes to U+FFFD
+    "bad_overlong_utf8": b"3\n1\n\xc0\xb0 1\n",  # overlong '0': malformed
+    "bad_truncated_utf8": b"3\n1\n1 \xd9",  # the last line ends inside a sequence
 }
+
+
+def malformed_bytes(case):
+    x = MALFORMED[case]
+    return x if isinstance(x, bytes) else x.encode()
 
 
 @pytest.mark.parametrize("case", sorted(MALFORMED))
 def test_parser_error_behaviour_matches_reference_semantics(tmp_path, case):
     bfsx = load_bfsx()
     p = tmp_path / f"{case}.txt"
-    p.write_bytes(MALFORMED[case].encode())
+    p.write_bytes(malformed_bytes(case))
     try:
         got = bfsx.parse_algs4(str(p))
         got_rc = 0
@@ -109,3 +127,22 @@ def test_init_without_gpu_fails_loudly():
     with pytest.raises(bfsx.BfsxError) as ei:
         bfsx.Context(0)
     assert ei.value.code == bfsx.BFSX_E_NODEV
+
+
+def test_unicode_digits_known_answers(tmp_path):
+    """Known answers of Integer.parseInt on non-ASCII digits (java.lang.Character.digit docs: a char of
+    category DECIMAL_DIGIT_NUMBER has its Unicode digit value): "١٢" = 12, "＋" is not a sign, and
+    fullwidth "１０" = 10."""
+    bfsx = load_bfsx()
+    p = tmp_path / "u.txt"
+    p.write_bytes("١٢\n0\n１０ १२\n".encode())  # V = 12; edge 10 - 12? no: 12 == V
+    with pytest.raises(bfsx.BfsxError) as ei:
+        bfsx.parse_algs4(str(p))
+    assert ei.value.code == bfsx.BFSX_E_RANGE  # "१२" = 12 is outside [0, 12)
+    p.write_bytes("١٣\n0\n１０ १२\n".encode())  # V = 13
+    nv, u, v = bfsx.parse_algs4(str(p))
+    assert nv == 13 and u.tolist() == [10] and v.tolist() == [12]
+    p.write_bytes("3\n0\n＋1 0\n".encode())  # fullwidth plus sign: not a sign, not a digit
+    with pytest.raises(bfsx.BfsxError) as ei:
+        bfsx.parse_algs4(str(p))
+    assert ei.value.code == bfsx.BFSX_E_PARSE

@@ -10,7 +10,7 @@ import pytest
 
 import oracle_py as O
 from conftest import GOLDEN
-from test_abi import MALFORMED
+from test_abi import MALFORMED, malformed_bytes
 
 pytestmark = pytest.mark.gpu
 
@@ -38,7 +38,7 @@ def test_gpu_parse_reference_files(bfsx, ctx, name):
 @pytest.mark.parametrize("case", sorted(MALFORMED))
 def test_gpu_parse_malformed_like_host(bfsx, ctx, tmp_path, case):
     p = tmp_path / f"{case}.txt"
-    p.write_bytes(MALFORMED[case].encode())
+    p.write_bytes(malformed_bytes(case))
     (rc_h, h, msg_h), (rc_g, g, msg_g) = both(bfsx, ctx, str(p))
     assert rc_h == rc_g
     if rc_h == 0:
