@@ -497,6 +497,23 @@ def test_hybrid_levels(ctx, bits, relabel):
                     check_against_oracle(g, nv, off, col, s, u, v, mr=False)
                     assert g.validate()["errors"] == 0
                     hy += sum(1 for d in g.level_dirs() if d == 3)
+        # leaf-heavy: 40 hubs on a ring, each with 300 degree-1 feet and links to 8 other hubs (the
+        # frontier after a hub level is almost all leaves, the case round 1's leaf filter faulted on)
+        rng = np.random.default_rng(77)
+        hubs = np.arange(40)
+        feet_u = np.repeat(hubs, 300)
+        feet_v = 40 + np.arange(40 * 300)
+        hl_u = np.repeat(hubs, 8)
+        hl_v = rng.integers(0, 40, hl_u.size)
+        u = np.concatenate([feet_u, hl_u, hubs]).astype(np.uint32)
+        v = np.concatenate([feet_v, hl_v, (hubs + 1) % 40]).astype(np.uint32)
+        nv = 40 + 40 * 300
+        off, col = O.build_sets(nv, u, v)
+        with ctx.from_edges(nv, u, v) as g:
+            for s in (0, 41, nv - 1):
+                check_against_oracle(g, nv, off, col, s, u, v, mr=False)
+                assert g.validate()["errors"] == 0
+                hy += sum(1 for d in g.level_dirs() if d == 3)
         ou, ov = O.kronecker(14, 16, 0x5EED2026)
         off, col = O.build_sets(1 << 14, ou, ov)
         for persist in ("off", "on"):
