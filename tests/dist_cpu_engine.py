@@ -1,7 +1,7 @@
-"""numpy model of one rank's libbfsx partition, for CPU (gloo) tests of bfsx_dist.DistBFS.
+"""numpy model of one rank's libbfsx partition, for CPU (gloo) tests of dist_driver.DistBFS.
 
 TEST INFRASTRUCTURE ONLY.  It implements the same level primitives as the GPU engine
-(bfsx_dist.GpuEngine -> libbfsx bfsx_dist_*), with the same data contracts:
+(dist_driver.GpuEngine -> libbfsx bfsx_dist_*), with the same data contracts:
   - partition: chunk = ceil(nv / P) rounded up to 64, rank r owns global ids [r*chunk, +chunk)
   - td_expand: claims owned targets, returns per-destination counts of (v << 32 | parent) pairs
     written to self.send grouped by owner in rank order

@@ -1,4 +1,9 @@
-"""Multi-GPU BFS driver: 1-D vertex partition, one process per GPU, exchange over torch.distributed.
+"""Test infrastructure: a Python restatement of the partitioned level loop over libbfsx's level
+primitives (bfsx_dist_begin / td_expand / td_claim / frontier_slice / bu_step / level_end / finish),
+with the exchange over torch.distributed.  The product loop is the native bfsx_dist_bfs
+(csrc/kernels_bfs.hip dist_bfs_run over csrc/bfsx_comm.cpp); this driver is the protocol reference the
+CPU (gloo, numpy engine) and GPU tests compare it with, and shows how a caller with its own exchange
+drives the primitives.  1-D vertex partition, one process per GPU.
 
 Replaces the reference's only collective -- Spark's hash-partitioned reduceByKey shuffle of whole
 Vertex objects, every level (BfsSpark.java:90) -- with an owner-routed exchange:

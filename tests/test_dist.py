@@ -1,4 +1,4 @@
-"""Multi-GPU driver (bfsx_dist.DistBFS) on CPU: world_size-2/3 gloo process groups, each rank a
+"""Python level-primitive driver (tests/dist_driver.py DistBFS) on CPU: world_size-2/3 gloo process groups, each rank a
 numpy partition engine (tests/dist_cpu_engine.py).  Checks the 1-D partition + owner-routed
 exchange protocol end to end: distances bit-exact against the oracle, parent trees valid, level
 count = the reference's pass count, m_comp equal to the oracle's."""
@@ -33,7 +33,7 @@ def _worker(rank, world, port, nv, u, v, sources, direction, q):
 
     from dist_cpu_engine import CpuEngine
 
-    spec = importlib.util.spec_from_file_location("bfsx_dist", os.path.join(PKG, "bfsx_dist.py"))
+    spec = importlib.util.spec_from_file_location("dist_driver", os.path.join(ROOT, "tests", "dist_driver.py"))
     bd = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bd)
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -29,12 +29,16 @@ def _free_port():
     return p
 
 
-def _load(name, file):
-    spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, file))
+def _load(name, file, where=PKG):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(where, file))
     mod = importlib.util.module_from_spec(spec)
     sys.modules[name] = mod
     spec.loader.exec_module(mod)
     return mod
+
+
+def _load_test(name, file):
+    return _load(name, file, os.path.dirname(os.path.abspath(__file__)))
 
 
 def _worker(rank, world, port, backend, graph, sources, direction, q):
@@ -43,7 +47,7 @@ def _worker(rank, world, port, backend, graph, sources, direction, q):
     import torch.distributed as dist
 
     bfsx = _load("bfsx", "bfsx.py")
-    bd = _load("bfsx_dist", "bfsx_dist.py")
+    bd = _load_test("dist_driver", "dist_driver.py")
     dist.init_process_group(backend, rank=rank, world_size=world)
     ctx = bfsx.Context(0)
     try:
