@@ -342,6 +342,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "bu_phased must be on|off");
         return BFSX_OK;
     }
+    if (k == "bu_lds_prefix") {
+        if (v == "on") ctx->opt.bu_lds_prefix = true;
+        else if (v == "off") ctx->opt.bu_lds_prefix = false;
+        else return fail(BFSX_E_ARG, "bu_lds_prefix must be on|off");
+        return BFSX_OK;
+    }
     if (k == "build_chunk") {
         char *end = nullptr;
         const long long x = strtoll(value, &end, 10);

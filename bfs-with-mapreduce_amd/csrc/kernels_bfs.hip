@@ -1341,19 +1341,35 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 
 // A2 then runs over that compacted list with every lane busy, compacting again for B.  The in-place
 // compaction only ever writes list slots the wave has already read (a round writes at most as many
 // entries as it consumed, at positions below its own), so no second list is needed.
+constexpr uint32_t kPrefIds = 1u << 16; // 8 KiB of LDS per workgroup
 template <class OffT, bool kMf, bool kHubs, bool kHubOnly>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu_ph(
     const OffT *__restrict__ row_off, const uint32_t *__restrict__ col, const uint32_t *__restrict__ top1,
     const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next, u64 *__restrict__ vis,
     u64 *__restrict__ stt, LevelSlot *ring, int level, int64_t nwords, uint32_t fmask,
-    const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, Published *pub,
-    u64 seq) {
+    const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t plim,
+    Published *pub, u64 seq) {
     constexpr int kU = 4;
     constexpr uint32_t kRound = 64 * kU;
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
     __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
+    // the frontier bits of the ids below plim (<= kPrefIds: the highest-degree vertices of a relabelled
+    // graph, where most probes land) copied to LDS once per workgroup
+    __shared__ uint32_t s_pref[kPrefIds / 32];
+    const uint32_t *front32 = reinterpret_cast<const uint32_t *>(front);
+    for (uint32_t i = threadIdx.x; i < plim / 32u; i += kBS) s_pref[i] = front32[i];
+    __syncthreads();
+    // the 32-bit frontier word of probe id x (x: plain id; kHubs graphs pass plim = 0)
+    auto fword = [&](uint32_t x) -> uint32_t {
+        if (x < plim) return s_pref[x >> 5];
+        return reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, x))[(x >> 5) & 1u];
+    };
+    auto fbit = [&](uint32_t x) -> uint32_t {
+        if (kHubOnly && !hub_entry<kHubs>(x, hub_lim)) return 0u;
+        return (fword(x) >> (x & 31u)) & 1u;
+    };
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
     uint32_t acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0;
@@ -1415,7 +1431,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                 for (int k = 0; k < kU; k++) {
                     const uint32_t xx = x[k] & ~fmask;
                     pw[k] = ((t0 + (uint32_t)k * 64 + lane < cnt) && (!kHubOnly || hub_entry<kHubs>(xx, hub_lim)))
-                                ? reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, xx))[(xx >> 5) & 1u]
+                                ? fword(xx)
                                 : 0u;
                 }
                 if (t0 + kRound < cnt) { // wave-uniform; issued behind the probes
@@ -1472,12 +1488,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                 uint32_t pbm = 0u; // bits 3k..3k+2: c1..c3 of candidate k in the frontier
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
-                    if (r[k].w != 0u) {
-                        pbm |= (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].x, hub_lim) |
-                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].y, hub_lim) << 1) |
-                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].z, hub_lim) << 2))
-                               << (3 * k);
-                    }
+                    if (r[k].w != 0u)
+                        pbm |= (fbit(r[k].x) | (fbit(r[k].y) << 1) | (fbit(r[k].z) << 2)) << (3 * k);
                 }
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
@@ -1519,10 +1531,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                         const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                         const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                         const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                        const uint32_t h0 = probe_hub<kHubs, kHubOnly>(front, hfront, x0, hub_lim);
-                        const uint32_t h1 = probe_hub<kHubs, kHubOnly>(front, hfront, x1, hub_lim);
-                        const uint32_t h2 = probe_hub<kHubs, kHubOnly>(front, hfront, x2, hub_lim);
-                        const uint32_t h3 = probe_hub<kHubs, kHubOnly>(front, hfront, x3, hub_lim);
+                        const uint32_t h0 = fbit(x0), h1 = fbit(x1), h2 = fbit(x2), h3 = fbit(x3);
                         if (h0 | h1 | h2 | h3) {
                             found = true;
                             const int hh = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
@@ -2129,9 +2138,14 @@ int launch_bu_ph(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64
                            ws->hub_id, ws->hub_k, front, ws->hfront);
         BFSX_HIP_TRY(hipGetLastError());
     }
+    // the LDS prefix: a relabelled single-device graph's highest-degree ids (off for the encoded hub
+    // domain, whose probe ids are not plain ids, and for partitions, whose hot ids start every range)
+    const uint32_t plim = (!kHubs && g->d_perm && g->nranks == 1 && g->ctx->opt.bu_lds_prefix)
+                              ? (uint32_t)std::min<int64_t>(kPrefIds, ws->nwords * 64) & ~63u
+                              : 0u;
     hipLaunchKernelGGL((k_bu_ph<OffT, kMf, kHubs, kHubOnly>), grid, dim3(kBS), 0, st, row_off,
                        kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring,
-                       level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, pub, seq);
+                       level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, plim, pub, seq);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
