@@ -336,12 +336,6 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "bu_pipeline must be on|off");
         return BFSX_OK;
     }
-    if (k == "bu_phased") {
-        if (v == "on") ctx->opt.bu_phased = true;
-        else if (v == "off") ctx->opt.bu_phased = false;
-        else return fail(BFSX_E_ARG, "bu_phased must be on|off");
-        return BFSX_OK;
-    }
     if (k == "bu_lds_prefix") {
         if (v == "on") ctx->opt.bu_lds_prefix = true;
         else if (v == "off") ctx->opt.bu_lds_prefix = false;

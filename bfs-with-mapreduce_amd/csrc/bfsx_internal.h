@@ -37,8 +37,7 @@ struct Options {
     int hub_bits = -1;          // bottom-up hub probe domain: -1 auto, 0 off, b = 2^b hubs
     int bu_unroll = 4;          // bottom-up candidates per lane per round (4 or 2)
     bool bu_pipeline = true;    // bottom-up: the next round's top1 loads overlap this round (kU = 4)
-    bool bu_phased = false;     // bottom-up: stage-major pull kernel (k_bu_ph) instead of round-major k_bu
-    bool bu_lds_prefix = true;  // k_bu_ph: the frontier bits of the 2^16 lowest (highest-degree) ids in LDS
+    bool bu_lds_prefix = true;  // pull kernels: the frontier bits of the 2^16 lowest (highest-degree) ids in LDS
     int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk

@@ -1117,19 +1117,36 @@ __device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *_
 // kPipe: the next round's top1 loads are issued right after this round's frontier probes, so they
 // overlap the probes, stage A2 and phase B instead of opening the next round (one dependent memory
 // latency fewer per round; a half-group of dense candidates runs up to 8 rounds).
+constexpr uint32_t kPrefIds = 1u << 16; // LDS frontier prefix: 8 KiB per workgroup
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 6 : (kU == 4 ? ((kMf && kPipe) ? 4 : 5) : 6)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
-                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, Published *pub,
-                                            u64 seq) {
+                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t plim,
+                                            Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
     __shared__ uint32_t s_miss[kWaves][(64 * kU)];
     __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
+    // the frontier bits of the ids below plim (<= kPrefIds: the highest-degree vertices of a relabelled
+    // graph, where most probes land) copied to LDS once per workgroup; plim = 0: off
+    __shared__ uint32_t s_pref[kPrefIds / 32];
+    {
+        const uint32_t *front32 = reinterpret_cast<const uint32_t *>(front);
+        for (uint32_t i = threadIdx.x; i < plim / 32u; i += kBS) s_pref[i] = front32[i];
+        __syncthreads();
+    }
+    auto fword = [&](uint32_t x) -> uint32_t { // 32-bit frontier word of probe id x
+        if (x < plim) return s_pref[x >> 5];
+        return reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, x))[(x >> 5) & 1u];
+    };
+    auto fbit = [&](uint32_t x) -> uint32_t {
+        if (kHubOnly && !hub_entry<kHubs>(x, hub_lim)) return 0u;
+        return (fword(x) >> (x & 31u)) & 1u;
+    };
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
     // per-lane counters fit 32 bits (a lane sees a few hundred candidates per launch); widened at the end
@@ -1198,7 +1215,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 
                 for (int k = 0; k < kU; k++) {
                     const uint32_t xx = x[k] & ~fmask;
                     pw[k] = ((t0 + (uint32_t)k * 64 + lane < he) && (!kHubOnly || hub_entry<kHubs>(xx, hub_lim)))
-                                ? reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, xx))[(xx >> 5) & 1u]
+                                ? fword(xx)
                                 : 0u;
                 }
                 if (kPipe && t1 < he) { // wave-uniform; issued after the probes, so waiting on them does not wait on these
@@ -1220,12 +1237,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 
                 uint32_t pbm = 0u; // bits 3k..3k+2: c1..c3 of candidate k in the frontier
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
-                    if (r[k].w != 0u) {
-                        pbm |= (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].x, hub_lim) |
-                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].y, hub_lim) << 1) |
-                                (probe_hub<kHubs, kHubOnly>(front, hfront, r[k].z, hub_lim) << 2))
-                               << (3 * k);
-                    }
+                    if (r[k].w != 0u)
+                        pbm |= (fbit(r[k].x) | (fbit(r[k].y) << 1) | (fbit(r[k].z) << 2)) << (3 * k);
                 }
                 uint32_t nmiss = 0; // wave-uniform
 #pragma unroll
@@ -1286,10 +1299,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 
                             const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                             const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                             const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                            const uint32_t h0 = probe_hub<kHubs, kHubOnly>(front, hfront, x0, hub_lim);
-                            const uint32_t h1 = probe_hub<kHubs, kHubOnly>(front, hfront, x1, hub_lim);
-                            const uint32_t h2 = probe_hub<kHubs, kHubOnly>(front, hfront, x2, hub_lim);
-                            const uint32_t h3 = probe_hub<kHubs, kHubOnly>(front, hfront, x3, hub_lim);
+                            const uint32_t h0 = fbit(x0), h1 = fbit(x1), h2 = fbit(x2), h3 = fbit(x3);
                             if (h0 | h1 | h2 | h3) {
                                 found = true;
                                 const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
@@ -1318,243 +1328,6 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
-            }
-            __builtin_amdgcn_wave_barrier(); // the next half rewrites the list
-        }
-        const u64 nxl = s_nx[wave][lane];
-        if (wl < nwords) {
-            next[wl] = nxl;
-            if (nxl) vis[wl] = vwl | nxl;
-        }
-    }
-    // claims field: rows walked (phase B)
-    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk);
-    publish_if_last(cn, pub, seq);
-}
-
-// Phase-major pull (option "bu_phased"): the same stages as k_bu, run stage by stage over a whole
-// half-group instead of round by round.  k_bu's round of 4 x 64 candidates waits for its slowest lane:
-// at a first pull level ~92% of the candidates settle on top1 (A1), so a round's A2 `rest` loads and
-// probes run for ~8% of its lanes and its phase B for a few, yet every round pays their latencies.
-// Here A1 sweeps all of the half-group's candidates (the next round's top1 loads in flight behind this
-// round's probes), compacting the candidates it cannot settle in place at the front of the LDS list;
-// A2 then runs over that compacted list with every lane busy, compacting again for B.  The in-place
-// compaction only ever writes list slots the wave has already read (a round writes at most as many
-// entries as it consumed, at positions below its own), so no second list is needed.
-constexpr uint32_t kPrefIds = 1u << 16; // 8 KiB of LDS per workgroup
-template <class OffT, bool kMf, bool kHubs, bool kHubOnly>
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu_ph(
-    const OffT *__restrict__ row_off, const uint32_t *__restrict__ col, const uint32_t *__restrict__ top1,
-    const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next, u64 *__restrict__ vis,
-    u64 *__restrict__ stt, LevelSlot *ring, int level, int64_t nwords, uint32_t fmask,
-    const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t plim,
-    Published *pub, u64 seq) {
-    constexpr int kU = 4;
-    constexpr uint32_t kRound = 64 * kU;
-    LevelSlot *cn = ring + (level + 1) % 3;
-    zero_slot(ring, level);
-    __shared__ u64 s_nx[kWaves][64];
-    __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
-    // the frontier bits of the ids below plim (<= kPrefIds: the highest-degree vertices of a relabelled
-    // graph, where most probes land) copied to LDS once per workgroup
-    __shared__ uint32_t s_pref[kPrefIds / 32];
-    const uint32_t *front32 = reinterpret_cast<const uint32_t *>(front);
-    for (uint32_t i = threadIdx.x; i < plim / 32u; i += kBS) s_pref[i] = front32[i];
-    __syncthreads();
-    // the 32-bit frontier word of probe id x (x: plain id; kHubs graphs pass plim = 0)
-    auto fword = [&](uint32_t x) -> uint32_t {
-        if (x < plim) return s_pref[x >> 5];
-        return reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, x))[(x >> 5) & 1u];
-    };
-    auto fbit = [&](uint32_t x) -> uint32_t {
-        if (kHubOnly && !hub_entry<kHubs>(x, hub_lim)) return 0u;
-        return (fword(x) >> (x & 31u)) & 1u;
-    };
-    const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    const int32_t nd = level + 1;
-    uint32_t acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0;
-    const int64_t wstride = (int64_t)gridDim.x * kWaves * 64;
-    // settle a found candidate: state, next-frontier bit (block-local LDS words), counters
-    auto settle = [&](uint32_t v, uint32_t par, uint32_t vbase) {
-        stt[v] = pack_state(probe_id<kHubs>(hub_id, par), nd);
-        atomicOr(&s_nx[wave][(v - vbase) >> 6], 1ull << (v & 63u));
-        acc_nf += 1;
-    };
-    for (int64_t w0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; w0 < nwords; w0 += wstride) {
-        const int64_t wl = w0 + lane;
-        const u64 vwl = wl < nwords ? vis[wl] : ~0ull;
-        const u64 unv = ~vwl;
-        const uint32_t c = (uint32_t)__popcll(unv);
-        const uint32_t incl = wave_incl_scan(c);
-        const uint32_t total = __shfl(incl, 63);
-        if (total == 0) { // wave-uniform: every vertex of the group visited or isolated
-            if (wl < nwords) next[wl] = 0ull;
-            continue;
-        }
-        const uint32_t excl = incl - c;
-        s_nx[wave][lane] = 0ull;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t vbase = (uint32_t)(w0 * 64);
-        const uint32_t half = __shfl(incl, 31); // candidates in words 0..31
-        for (int h = 0; h < 2; h++) {
-            const uint32_t hb = h ? half : 0u, cnt = (h ? total : half) - hb;
-            if (cnt == 0) continue; // wave-uniform
-            if ((lane >> 5) == (unsigned)h) {
-                u64 bits = unv;
-                uint32_t idx = excl - hb;
-                while (bits) {
-                    s_cand[wave][idx++] = (uint16_t)(lane * 64u + (uint32_t)(__ffsll((long long)bits) - 1));
-                    bits &= bits - 1ull;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            // ---- A1: top1 + its frontier bit for every candidate; the unsettled ones -> s_cand[0, n1)
-            uint32_t n1 = 0;
-            uint32_t xn[kU];
-#pragma unroll
-            for (int k = 0; k < kU; k++) {
-                const uint32_t at = (uint32_t)k * 64 + lane;
-                xn[k] = at < cnt ? top1[vbase + s_cand[wave][at]] : 0u;
-            }
-            for (uint32_t t0 = 0; t0 < cnt; t0 += kRound) {
-                uint32_t v[kU], x[kU], vn[kU];
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    const uint32_t at = t0 + (uint32_t)k * 64 + lane, an = at + kRound;
-                    v[k] = vbase + s_cand[wave][at < 2048u ? at : 0u]; // past the list: masked below
-                    vn[k] = vbase + s_cand[wave][an < 2048u ? an : 0u];
-                    x[k] = xn[k];
-                }
-                __builtin_amdgcn_wave_barrier(); // this round's and the next round's entries are read
-                uint32_t pw[kU];
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    const uint32_t xx = x[k] & ~fmask;
-                    pw[k] = ((t0 + (uint32_t)k * 64 + lane < cnt) && (!kHubOnly || hub_entry<kHubs>(xx, hub_lim)))
-                                ? fword(xx)
-                                : 0u;
-                }
-                if (t0 + kRound < cnt) { // wave-uniform; issued behind the probes
-#pragma unroll
-                    for (int k = 0; k < kU; k++)
-                        xn[k] = (t0 + kRound + (uint32_t)k * 64 + lane < cnt) ? top1[vn[k]] : 0u;
-                }
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    const bool ok = t0 + (uint32_t)k * 64 + lane < cnt;
-                    const uint32_t xx = x[k] & ~fmask;
-                    bool found = false, a2 = false;
-                    if (ok) {
-                        if ((pw[k] >> (xx & 31u)) & 1u) {
-                            found = true;
-                            acc_sc += 1;
-                        } else if ((x[k] & fmask) != 0u) { // top1 was the row's only entry
-                            acc_mu += 1;
-                            acc_sc += 1;
-                        } else if (kHubOnly && !hub_entry<kHubs>(xx, hub_lim)) {
-                            acc_mu += 1; // no hub in the row (the next pull level recounts m_u)
-                            acc_sc += 1;
-                        } else {
-                            a2 = true;
-                        }
-                    }
-                    if (found) {
-                        settle(v[k], xx, vbase);
-                        if (kMf) acc_mf += (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
-                    }
-                    const u64 mm = __ballot(a2);
-                    if (a2) s_cand[wave][n1 + __popcll(mm & ((1ull << lane) - 1ull))] = (uint16_t)(v[k] - vbase);
-                    n1 += (uint32_t)__popcll(mm);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            // ---- A2: rest[v] = {c1, c2, c3, deg} for the unsettled; rows longer than 4 -> s_cand[0, n2)
-            uint32_t n2 = 0;
-            for (uint32_t t0 = 0; t0 < n1; t0 += kRound) {
-                uint32_t v[kU];
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    const uint32_t at = t0 + (uint32_t)k * 64 + lane;
-                    v[k] = vbase + s_cand[wave][at < 2048u ? at : 0u];
-                }
-                __builtin_amdgcn_wave_barrier();
-                uint4 r[kU];
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    const bool ok = t0 + (uint32_t)k * 64 + lane < n1;
-                    r[k] = ok ? rest[v[k]] : make_uint4(0u, 0u, 0u, 0u);
-                    acc_s2 += ok;
-                }
-                uint32_t pbm = 0u; // bits 3k..3k+2: c1..c3 of candidate k in the frontier
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    if (r[k].w != 0u)
-                        pbm |= (fbit(r[k].x) | (fbit(r[k].y) << 1) | (fbit(r[k].z) << 2)) << (3 * k);
-                }
-#pragma unroll
-                for (int k = 0; k < kU; k++) {
-                    const bool ok = t0 + (uint32_t)k * 64 + lane < n1;
-                    const uint32_t deg = r[k].w, pb = (pbm >> (3 * k)) & 7u;
-                    bool miss = false;
-                    if (ok) {
-                        if (pb) {
-                            settle(v[k], (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z, vbase);
-                            acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
-                            if (kMf) acc_mf += deg;
-                        } else if (deg <= 4u || (kHubOnly && !(hub_entry<kHubs>(r[k].x, hub_lim) &&
-                                                               hub_entry<kHubs>(r[k].y, hub_lim) &&
-                                                               hub_entry<kHubs>(r[k].z, hub_lim)))) {
-                            acc_mu += deg; // row exhausted (or, hub sweep: its hub prefix is)
-                            acc_sc += deg < 4u ? deg : 4u;
-                        } else {
-                            miss = true;
-                            acc_sc += 4;
-                        }
-                    }
-                    const u64 mm = __ballot(miss);
-                    if (miss) s_cand[wave][n2 + __popcll(mm & ((1ull << lane) - 1ull))] = (uint16_t)(v[k] - vbase);
-                    n2 += (uint32_t)__popcll(mm);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            // ---- B: rows longer than 4 with no hit in their first 4 entries walk the rest, 4 per step
-            for (uint32_t m0 = 0; m0 < n2; m0 += 64) {
-                if (m0 + lane < n2) {
-                    const uint32_t vv = vbase + s_cand[wave][m0 + lane];
-                    const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
-                    bool found = false, stop = false;
-                    uint32_t par = 0;
-                    int64_t j = b + 4;
-                    while (!found && !stop && j < e) {
-                        const int64_t left = e - j;
-                        const uint32_t x0 = col[j];
-                        const uint32_t x1 = left > 1 ? col[j + 1] : x0;
-                        const uint32_t x2 = left > 2 ? col[j + 2] : x0;
-                        const uint32_t x3 = left > 3 ? col[j + 3] : x0;
-                        const uint32_t h0 = fbit(x0), h1 = fbit(x1), h2 = fbit(x2), h3 = fbit(x3);
-                        if (h0 | h1 | h2 | h3) {
-                            found = true;
-                            const int hh = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
-                            par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
-                            j += hh + 1;
-                        } else {
-                            j += left < 4 ? left : 4;
-                            // hub sweep: rows are degree-ordered, so past the first non-hub entry no hub follows
-                            if (kHubOnly)
-                                stop = !(hub_entry<kHubs>(x0, hub_lim) && hub_entry<kHubs>(x1, hub_lim) &&
-                                         hub_entry<kHubs>(x2, hub_lim) && hub_entry<kHubs>(x3, hub_lim));
-                        }
-                    }
-                    acc_sc += (uint32_t)(j - b - 4);
-                    acc_wk += (uint32_t)(j - b - 4);
-                    acc_rows += 1;
-                    if (found) {
-                        settle(vv, par, vbase);
-                        if (kMf) acc_mf += (uint32_t)(e - b);
-                    } else {
-                        acc_mu += (uint32_t)(e - b);
-                    }
-                }
             }
             __builtin_amdgcn_wave_barrier(); // the next half rewrites the list
         }
@@ -2092,6 +1865,15 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     return BFSX_OK;
 }
 
+// Frontier ids whose bits the pull kernels read from an LDS copy: a relabelled single-device graph's
+// highest-degree ids (off for the encoded hub domain, whose probe ids are not plain ids, and for
+// partitions, whose hot ids start every range).
+template <bool kHubs>
+uint32_t lds_prefix_ids(const bfsx_graph *g, const BfsWorkspace *ws) {
+    if (kHubs || !g->d_perm || g->nranks != 1 || !g->ctx->opt.bu_lds_prefix) return 0u;
+    return (uint32_t)std::min<int64_t>(kPrefIds, ws->nwords * 64) & ~63u;
+}
+
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
 int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
                 u64 seq) {
@@ -2114,38 +1896,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     }
     hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
                        ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
-                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, pub, seq);
-    BFSX_HIP_TRY(hipGetLastError());
-    return BFSX_OK;
-}
-
-// The phase-major variant (k_bu_ph), same grid rule as launch_bu_u.
-template <class OffT, bool kMf, bool kHubs, bool kHubOnly>
-int launch_bu_ph(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
-                 u64 seq) {
-    hipStream_t st = g->ctx->stream;
-    static int per_cu = 0;
-    if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu_ph<OffT, kMf, kHubs, kHubOnly>, kBS, 0) !=
-                hipSuccess ||
-            per_cu < 1)
-            per_cu = 4;
-    }
-    const unsigned cap = (unsigned)(g->ctx->num_cus * per_cu);
-    const dim3 grid(clamp_grid((ws->nwords + kWaves * 64 - 1) / (kWaves * 64), cap));
-    if (kHubs) {
-        hipLaunchKernelGGL(k_hub_gather, dim3(clamp_grid((ws->hub_k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                           ws->hub_id, ws->hub_k, front, ws->hfront);
-        BFSX_HIP_TRY(hipGetLastError());
-    }
-    // the LDS prefix: a relabelled single-device graph's highest-degree ids (off for the encoded hub
-    // domain, whose probe ids are not plain ids, and for partitions, whose hot ids start every range)
-    const uint32_t plim = (!kHubs && g->d_perm && g->nranks == 1 && g->ctx->opt.bu_lds_prefix)
-                              ? (uint32_t)std::min<int64_t>(kPrefIds, ws->nwords * 64) & ~63u
-                              : 0u;
-    hipLaunchKernelGGL((k_bu_ph<OffT, kMf, kHubs, kHubOnly>), grid, dim3(kBS), 0, st, row_off,
-                       kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring,
-                       level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, plim, pub, seq);
+                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, lds_prefix_ids<kHubs>(g, ws), pub, seq);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -2153,7 +1904,6 @@ int launch_bu_ph(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64
 template <class OffT, bool kMf, bool kHubs>
 int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
                 u64 seq) {
-    if (g->ctx->opt.bu_phased) return launch_bu_ph<OffT, kMf, kHubs, false>(g, ws, row_off, front, level, pub, seq);
     if (g->ctx->opt.bu_unroll == 2) return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, level, pub, seq);
     // kMf (partitioned) + kPipe needs more than the 96 VGPRs of 5 waves per SIMD: that instantiation runs
     // at 4 waves per SIMD (a spilling pull kernel is never an option)

@@ -110,6 +110,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "bu_unroll" = 4|2 (bottom-up candidates per lane per round)
  *   "bu_pipeline" = on|off (bottom-up: the next round's first-neighbour loads overlap the current round;
  *                 with bu_unroll 4; default on)
+ *   "bu_lds_prefix" = on|off (pull kernels read the frontier bits of the 2^16 highest-degree ids of a
+ *                 relabelled single-device graph from a per-workgroup LDS copy; default on)
  *   "slot_pairs" = int (partitioned graphs: a push level whose frontier has at most this many edges in
  *                 total exchanges its pairs through fixed per-peer slots, skipping the count all-to-all
  *                 and its host wait; default 16384, 0 = never)

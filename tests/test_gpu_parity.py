@@ -445,14 +445,14 @@ def test_chunked_csr_build(ctx, chunk, relabel):
 
 
 @pytest.mark.parametrize("relabel", ["on", "off"])
-@pytest.mark.parametrize("unroll", ["2", "4", "4-nopipe", "phased"])
+@pytest.mark.parametrize("unroll", ["2", "4", "4-nopipe", "4-noprefix"])
 def test_bottomup_unroll_variants(ctx, unroll, relabel):
-    """Every pull kernel instantiation (k_bu with 2 or 4 candidates per lane per round; with 4, the next
-    round's top1 loads pipelined or not; the stage-major k_bu_ph) is bit-exact, pull-only and
-    direction-optimising, with and without hubs."""
-    ctx.set_option("bu_phased", "on" if unroll == "phased" else "off")
-    ctx.set_option("bu_unroll", "4" if unroll == "phased" else unroll.split("-")[0])
+    """Every k_bu instantiation (2 or 4 candidates per lane per round; with 4, the next round's top1
+    loads pipelined or not; the LDS copy of the hub prefix's frontier bits on or off) is bit-exact,
+    pull-only and direction-optimising, with and without hubs."""
+    ctx.set_option("bu_unroll", unroll.split("-")[0])
     ctx.set_option("bu_pipeline", "off" if unroll.endswith("nopipe") else "on")
+    ctx.set_option("bu_lds_prefix", "off" if unroll.endswith("noprefix") else "on")
     ctx.set_option("relabel", relabel)
     try:
         for hub in ("off", "auto"):
@@ -472,7 +472,7 @@ def test_bottomup_unroll_variants(ctx, unroll, relabel):
                         check_against_oracle(g, 1 << 16, off, col, int(r), ou, ov, mr=False)
     finally:
         for k, val in (("bu_unroll", "4"), ("bu_pipeline", "on"), ("relabel", "on"), ("hub_bits", "auto"),
-                       ("direction", "auto"), ("bu_phased", "off")):
+                       ("direction", "auto"), ("bu_lds_prefix", "on")):
             ctx.set_option(k, val)
 
 
