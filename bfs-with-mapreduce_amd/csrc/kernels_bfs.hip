@@ -1118,29 +1118,41 @@ __device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *_
 // overlap the probes, stage A2 and phase B instead of opening the next round (one dependent memory
 // latency fewer per round; a half-group of dense candidates runs up to 8 rounds).
 constexpr uint32_t kPrefIds = 1u << 16; // LDS frontier prefix: 8 KiB per workgroup
+// The ids whose frontier bits the pull kernel reads from LDS: the first `ids` ids of each of `nseg` id
+// ranges of 2^shift ids (one range on one device, shift >= 32 = the whole id space; a partition's
+// ranks' ranges).  ids = 0: off.
+struct PrefixSpec {
+    uint32_t ids, nseg, shift, pad;
+};
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 6 : (kU == 4 ? ((kMf && kPipe) ? 4 : 5) : 6)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
-                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t plim,
+                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, PrefixSpec pf,
                                             Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
     __shared__ uint32_t s_miss[kWaves][(64 * kU)];
     __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
-    // the frontier bits of the ids below plim (<= kPrefIds: the highest-degree vertices of a relabelled
-    // graph, where most probes land) copied to LDS once per workgroup; plim = 0: off
+    // the frontier bits of the first pf.ids ids of every id range (the highest-degree vertices of a
+    // relabelled graph, where most probes land) copied to LDS once per workgroup; pf.ids = 0: off
     __shared__ uint32_t s_pref[kPrefIds / 32];
     {
         const uint32_t *front32 = reinterpret_cast<const uint32_t *>(front);
-        for (uint32_t i = threadIdx.x; i < plim / 32u; i += kBS) s_pref[i] = front32[i];
+        const uint32_t wps = pf.ids / 32u; // words per range
+        for (uint32_t i = threadIdx.x; i < wps * pf.nseg; i += kBS) {
+            const uint32_t seg = i / wps;
+            s_pref[i] = front32[((size_t)seg << (pf.shift - 5)) + (i - seg * wps)];
+        }
         __syncthreads();
     }
     auto fword = [&](uint32_t x) -> uint32_t { // 32-bit frontier word of probe id x
-        if (x < plim) return s_pref[x >> 5];
+        const uint32_t seg = pf.shift >= 32 ? 0u : (x >> pf.shift);
+        const uint32_t off = pf.shift >= 32 ? x : (x & ((1u << pf.shift) - 1u));
+        if (off < pf.ids) return s_pref[seg * (pf.ids >> 5) + (off >> 5)];
         return reinterpret_cast<const uint32_t *>(probe_word<kHubs>(front, hfront, x))[(x >> 5) & 1u];
     };
     auto fbit = [&](uint32_t x) -> uint32_t {
@@ -1865,13 +1877,21 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     return BFSX_OK;
 }
 
-// Frontier ids whose bits the pull kernels read from an LDS copy: a relabelled single-device graph's
-// highest-degree ids (off for the encoded hub domain, whose probe ids are not plain ids, and for
-// partitions, whose hot ids start every range).
+// Frontier ids whose bits the pull kernels read from an LDS copy: the highest-degree ids of a
+// relabelled graph -- on one device the first 2^16 ids, on a partition the first 2^16/P ids of every
+// rank's range (its own hubs) when the ranges are powers of two.  Off for the encoded hub domain, whose
+// probe ids are not plain ids.
 template <bool kHubs>
-uint32_t lds_prefix_ids(const bfsx_graph *g, const BfsWorkspace *ws) {
-    if (kHubs || !g->d_perm || g->nranks != 1 || !g->ctx->opt.bu_lds_prefix) return 0u;
-    return (uint32_t)std::min<int64_t>(kPrefIds, ws->nwords * 64) & ~63u;
+PrefixSpec lds_prefix(const bfsx_graph *g, const BfsWorkspace *ws) {
+    PrefixSpec off{0u, 0u, 32u, 0u};
+    if (kHubs || !g->d_perm || !g->ctx->opt.bu_lds_prefix) return off;
+    if (g->nranks == 1) return PrefixSpec{(uint32_t)std::min<int64_t>(kPrefIds, ws->nwords * 64) & ~63u, 1u, 32u, 0u};
+    const int64_t chunk = g->chunk;
+    if (chunk & (chunk - 1)) return off; // not a power of two: the range of an id would need a division
+    int shift = 0;
+    while (((int64_t)1 << shift) < chunk) shift++;
+    const uint32_t per = (uint32_t)std::min<int64_t>(kPrefIds / g->nranks, chunk) & ~63u;
+    return per ? PrefixSpec{per, (uint32_t)g->nranks, (uint32_t)shift, 0u} : off;
 }
 
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
@@ -1896,7 +1916,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     }
     hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
                        ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
-                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, lds_prefix_ids<kHubs>(g, ws), pub, seq);
+                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, lds_prefix<kHubs>(g, ws), pub, seq);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
