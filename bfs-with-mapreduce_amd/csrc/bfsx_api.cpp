@@ -278,6 +278,7 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         return BFSX_OK;
     }
     if (k == "alpha") return as_int(ctx->opt.alpha);
+    if (k == "hybrid_pct") return as_int(ctx->opt.hybrid_pct);
     if (k == "beta") return as_int(ctx->opt.beta);
     if (k == "persist") {
         if (v == "on") ctx->opt.persist = true;

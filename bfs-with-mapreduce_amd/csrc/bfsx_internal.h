@@ -40,6 +40,7 @@ struct Options {
     bool bu_lds_prefix = true;  // pull kernels: the frontier bits of the 2^16 lowest (highest-degree) ids in LDS
     int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
+    int hybrid_pct = 125;       // auto: hybrid when the frontier's hub edges exceed this % of the unvisited count
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
     int persist_abort_at = -1;  // test hook: K3p aborts at this level of its launch (-1: never)
     int64_t persist_dmax = 2048; // K3p only while every frontier vertex has at most this degree

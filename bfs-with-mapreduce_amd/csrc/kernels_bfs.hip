@@ -2232,7 +2232,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         bool hybrid = false;
         if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && has_hubs(ws) && opt.hybrid != 0 && mfh > 0) {
             const int64_t unv = nv - visited - ws->n_dead;
-            hybrid = opt.hybrid == 2 || 4 * mfh > 5 * unv;
+            hybrid = opt.hybrid == 2 || 100 * mfh > (int64_t)opt.hybrid_pct * unv;
         }
         if (hybrid) {
             BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));

@@ -107,6 +107,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 gathered bitmap; auto = n/1024 rounded up to a power of two; fixed at a graph's first BFS)
  *   "hybrid" = auto|off|force (a top-down level whose frontier's edges sit mostly in hub-domain vertices
  *                 runs as pull-from-hubs + push-from-the-rest; force = every eligible level, for tests)
+ *   "hybrid_pct" = int (auto: a level goes hybrid when its frontier's hub edges exceed this percentage
+ *                 of the unvisited vertex count; default 125)
  *   "bu_unroll" = 4|2 (bottom-up candidates per lane per round)
  *   "bu_pipeline" = on|off (bottom-up: the next round's first-neighbour loads overlap the current round;
  *                 with bu_unroll 4; default on)
