@@ -1125,7 +1125,7 @@ struct PrefixSpec {
     uint32_t ids, nseg, shift, pad;
 };
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(kHubOnly ? 6 : (kU == 4 ? ((kMf && kPipe) ? 4 : 5) : 6)))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
