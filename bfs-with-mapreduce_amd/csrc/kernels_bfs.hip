@@ -1311,19 +1311,28 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                             const uint32_t x1 = left > 1 ? col[j + 1] : x0;
                             const uint32_t x2 = left > 2 ? col[j + 2] : x0;
                             const uint32_t x3 = left > 3 ? col[j + 3] : x0;
+                            const uint32_t x4 = left > 4 ? col[j + 4] : x0;
+                            const uint32_t x5 = left > 5 ? col[j + 5] : x0;
+                            const uint32_t x6 = left > 6 ? col[j + 6] : x0;
+                            const uint32_t x7 = left > 7 ? col[j + 7] : x0;
                             const uint32_t h0 = fbit(x0), h1 = fbit(x1), h2 = fbit(x2), h3 = fbit(x3);
-                            if (h0 | h1 | h2 | h3) {
+                            const uint32_t h4 = fbit(x4), h5 = fbit(x5), h6 = fbit(x6), h7 = fbit(x7);
+                            const uint32_t hm = h0 | (h1 << 1) | (h2 << 2) | (h3 << 3) | (h4 << 4) | (h5 << 5) |
+                                                (h6 << 6) | (h7 << 7);
+                            if (hm) {
                                 found = true;
-                                const int h = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
-                                par = h0 ? x0 : h1 ? x1 : h2 ? x2 : x3;
+                                const int h = __ffs((int)hm) - 1;
+                                par = h == 0 ? x0 : h == 1 ? x1 : h == 2 ? x2 : h == 3 ? x3 : h == 4 ? x4 : h == 5 ? x5 : h == 6 ? x6 : x7;
                                 j += h + 1;
                             } else {
-                                j += left < 4 ? left : 4;
+                                j += left < 8 ? left : 8;
                                 // hub sweep: rows are degree-ordered, so past the first non-hub entry no
                                 // hub follows
                                 if (kHubOnly)
                                     stop = !(hub_entry<kHubs>(x0, hub_lim) && hub_entry<kHubs>(x1, hub_lim) &&
-                                             hub_entry<kHubs>(x2, hub_lim) && hub_entry<kHubs>(x3, hub_lim));
+                                             hub_entry<kHubs>(x2, hub_lim) && hub_entry<kHubs>(x3, hub_lim) &&
+                                             hub_entry<kHubs>(x4, hub_lim) && hub_entry<kHubs>(x5, hub_lim) &&
+                                             hub_entry<kHubs>(x6, hub_lim) && hub_entry<kHubs>(x7, hub_lim));
                             }
                         }
                         acc_sc += (uint32_t)(j - b - 4);
