@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ 
 //   A  every lane takes kBuU candidates at once: kBuU coalesced top1[v] loads (v's highest-degree
 //      neighbour), then kBuU independent frontier-bit probes -- the whole round costs two memory
 //      round trips instead of two per candidate.  Hits are done: no row offset is ever read for them.
-//   B  the misses (compacted into LDS with a ballot) walk the rest of their rows, 4 entries per step.
+//   B  the misses (compacted into LDS with a ballot) walk the rest of their rows, 8 entries per step.
 //      A miss whose row holds only top1 (kDeg1 flag in top1) is settled in A without a row read.
 // Found bits are OR-ed into a per-wave LDS copy of the 64 next-frontier words and written back
 // coalesced with the visited words.  Single GPU: m_f of the new frontier is not needed (a bottom-up
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                     nmiss += (uint32_t)__popcll(mm);
                 }
                 __builtin_amdgcn_wave_barrier();
-                // B: rows longer than 4 with no hit in their first 4 entries walk the rest, 4 per step
+                // B: rows longer than 4 with no hit in their first 4 entries walk the rest, 8 per step
                 for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
                     if (m0 + lane < nmiss) {
                         const uint32_t vv = s_miss[wave][m0 + lane];
