@@ -318,6 +318,20 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.slot_pairs = x;
         return BFSX_OK;
     }
+    if (k == "leaf_skip") {
+        if (v == "on") ctx->opt.leaf_skip = true;
+        else if (v == "off") ctx->opt.leaf_skip = false;
+        else return fail(BFSX_E_ARG, "leaf_skip must be on|off");
+        return BFSX_OK;
+    }
+    if (k == "big_degree" || k == "big_cap") {
+        char *end = nullptr;
+        const long long x = strtoll(value, &end, 10);
+        if (!end || *end || x < (k == "big_cap" ? 1 : 0) || x > 0xFFFFFFFFll)
+            return fail(BFSX_E_ARG, k + " must be an integer in [" + (k == "big_cap" ? "1" : "0") + ", 2^32)");
+        (k == "big_cap" ? ctx->opt.big_cap : ctx->opt.big_degree) = x;
+        return BFSX_OK;
+    }
     if (k == "hybrid") {
         if (v == "off") ctx->opt.hybrid = 0;
         else if (v == "auto") ctx->opt.hybrid = 1;

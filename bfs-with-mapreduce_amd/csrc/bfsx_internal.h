@@ -39,6 +39,11 @@ struct Options {
     bool bu_pipeline = true;    // bottom-up: the next round's top1 loads overlap this round (kU = 4)
     bool bu_lds_prefix = true;  // pull kernels: the frontier bits of the 2^16 lowest (highest-degree) ids in LDS
     int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
+    // partitioned: ids of degree above big_degree (at most big_cap per rank) are listed with their degree
+    // on every rank (read at a graph's first partitioned BFS; see dist_big_list)
+    int64_t big_degree = 4096;
+    bool leaf_skip = true;      // single device: a pull level's degree-1 discoveries stay out of the next push queue
+    int64_t big_cap = (int64_t)1 << 20;
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
     int hybrid_pct = 125;       // auto: hybrid when the frontier's hub edges exceed this % of the unvisited count
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk

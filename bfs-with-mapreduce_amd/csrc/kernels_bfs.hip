@@ -104,6 +104,10 @@ struct BfsWorkspace {
     // relabelled graph (ids in degree order): the hubs of the hybrid levels are the ids below hub_lim and
     // need no encoded domain (their frontier bits are already the first hub_lim/64 words of the bitmap)
     uint32_t hub_lim = 0;
+    // every id >= leaf_lo has at most one adjacency entry (on a relabelled graph the degree-1 tail): a
+    // discovered leaf's only neighbour is its parent, so a push level after a pull level leaves the
+    // leaves of its bitmap frontier out of its queue (option leaf_skip)
+    int64_t leaf_lo = 0;
     uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
     u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
@@ -135,7 +139,11 @@ struct BfsWorkspace {
     u64 *sendbuf = nullptr, *recvbuf = nullptr, *fglob = nullptr; // native exchange buffers
     int64_t send_cap = 0, recv_cap = 0, fglob_words = 0;
     int64_t nnz_global = -1;
-    std::vector<uint32_t> h_gdeg;       // partitioned: global degree of every id (rank p's slice at p * chunk)
+    // partitioned: the ORIGINAL ids whose degree exceeds big_thr, sorted, with their degrees (u64 id << 32 |
+    // degree), all-gathered once per graph; every other id has degree <= big_thr (see dist_bfs_run)
+    std::vector<u64> h_big;
+    int64_t big_thr = -1;               // -1: not built; the slot_pairs option the list was built for
+    bool big_overflow = false;          // more than big_cap such ids on a rank: source degrees unknown (counted level 0)
     int d_level = 0, d_dir = BFSX_DIR_TOPDOWN;
     bool d_in_queue = true;
     int64_t d_nf = 0, d_mf = 0;
@@ -1130,8 +1138,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
-                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, PrefixSpec pf,
-                                            Published *pub, u64 seq) {
+                                            const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo,
+                                            PrefixSpec pf, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
@@ -1291,6 +1299,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
                         if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
+                        else if (!kHubOnly) acc_mf += v[k] < leaf_lo ? 1u : 0u; // single device: non-leaves found
                     }
                     const u64 mm = __ballot(miss);
                     if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
@@ -1343,6 +1352,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
                             if (kMf) acc_mf += (uint32_t)(e - b);
+                            else if (!kHubOnly) acc_mf += vv < leaf_lo ? 1u : 0u;
                         } else {
                             acc_mu += (uint32_t)(e - b);
                         }
@@ -1397,9 +1407,10 @@ __global__ __launch_bounds__(kBS) void k_new_bits(const u64 *__restrict__ vis, i
 // reservation counter sees a few hundred arrivals, not one per wave.
 constexpr int kCompactWords = 16;
 
+// lim: ids >= lim are left out (the leaves of leaf_skip); nwords covers them at most by one word.
 __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const u64 *__restrict__ bm, int64_t nwords,
                                                          int64_t words_per_block, uint32_t *__restrict__ q,
-                                                         u64 *cursor) {
+                                                         u64 *cursor, int64_t lim) {
     __shared__ uint32_t s_wsum[kWaves];
     __shared__ uint32_t s_base;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
@@ -1412,6 +1423,7 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const u64 *__restrict__
         for (int i = 0; i < kCompactWords; i++) {
             const int64_t w = w0 + (int64_t)i * kBS + tid;
             x[i] = w < we ? bm[w] : 0ull;
+            if (w * 64 + 64 > lim) x[i] &= w * 64 >= lim ? 0ull : (1ull << (lim - w * 64)) - 1ull;
             c += (uint32_t)__popcll(x[i]);
         }
         const uint32_t inc = wave_incl_scan(c);
@@ -1510,6 +1522,18 @@ __global__ __launch_bounds__(kBS) void k_top1(const int64_t *__restrict__ row_of
     }
 }
 
+// *out = 1 + the largest row id with two or more adjacency entries (0: none)
+__global__ __launch_bounds__(kBS) void k_leaf_lo(const int64_t *__restrict__ row_off, int64_t nv, u64 *out) {
+    u64 m = 0;
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS)
+        if (row_off[v + 1] - row_off[v] >= 2) m = (u64)v + 1;
+    for (int d = 32; d >= 1; d >>= 1) {
+        const u64 o = __shfl_xor(m, d);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63u) == 0 && m) atomicMax(out, m);
+}
+
 // rest[v] = {c1, c2, c3, deg} of row v (see k_bu); rows shorter than 4 repeat their last entry
 // (a degree-1 row repeats top1: probing it again is harmless).
 __global__ __launch_bounds__(kBS) void k_rest(const int64_t *__restrict__ row_off, const uint32_t *__restrict__ col,
@@ -1534,6 +1558,18 @@ __global__ __launch_bounds__(kBS) void k_slice_degrees(const int64_t *__restrict
     for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < chunk; v += (int64_t)gridDim.x * kBS) {
         const int64_t r = (perm && v < nv) ? (int64_t)perm[v] : v;
         out[v] = v < nv ? (uint32_t)(row_off[r + 1] - row_off[r]) : 0u;
+    }
+}
+// The ids of a slice (original ids, slice-relative) whose degree exceeds thr, appended as (global id << 32 |
+// degree) to out[0..cap); *cnt counts all of them (a count above cap means the list overflowed).
+__global__ __launch_bounds__(kBS) void k_select_big(const uint32_t *__restrict__ deg, int64_t chunk, uint32_t thr,
+                                                    int64_t v_lo, u64 *__restrict__ out, u64 cap, u64 *cnt) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < chunk; v += (int64_t)gridDim.x * kBS) {
+        const uint32_t d = deg[v];
+        if (d > thr) {
+            const u64 i = atomicAdd(cnt, 1ull);
+            if (i < cap) out[i] = ((u64)(v_lo + v) << 32) | d;
+        }
     }
 }
 // Hub selection: sort keys ~degree (ascending = degree descending, ties by id: the sort is stable).
@@ -1827,14 +1863,17 @@ int ws_alloc(bfsx_graph *g) {
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
                        g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
     BFSX_HIP_TRY(hipGetLastError());
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(u64), st));
     hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
                        ws->nwords, ws->d_red);
     BFSX_HIP_TRY(hipGetLastError());
-    u64 nd = 0;
-    BFSX_HIP_TRY(hipMemcpyAsync(&nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(k_leaf_lo, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, ws->d_red + 1);
+    BFSX_HIP_TRY(hipGetLastError());
+    u64 nd[2] = {0, 0};
+    BFSX_HIP_TRY(hipMemcpyAsync(nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
-    ws->n_dead = (int64_t)nd - (ws->nwords * 64 - g->nv); // minus padding bits
+    ws->n_dead = (int64_t)nd[0] - (ws->nwords * 64 - g->nv); // minus padding bits
+    ws->leaf_lo = (int64_t)nd[1];
     return BFSX_OK;
 }
 
@@ -1925,7 +1964,8 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     }
     hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
                        ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
-                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim, lds_prefix<kHubs>(g, ws), pub, seq);
+                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim,
+                       (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws), pub, seq);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -2207,6 +2247,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // degree sum sits mostly in hubs runs as a hybrid level (below)
     int64_t mfh = ((ws->hub_k > 0 && mf >= (int64_t)ws->hub_tdeg) || source < (int64_t)ws->hub_lim) ? mf : 0;
     int64_t examined = 0, visited = 1;
+    // the frontier's vertices below leaf_lo (-1: unknown); set by a pull level (its k_bu counts them)
+    int64_t nf_core = -1;
     int td_levels = 0, bu_levels = 0;
     std::vector<LevelTiming> timing;
     g->level_dirs.clear();
@@ -2281,6 +2323,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             dmax = -1;
             mfh = -1;
             dir = BFSX_DIR_BOTTOMUP; // the new frontier is a bitmap
+            nf_core = -1;
             in_queue = false;
             snapped = false;
             bu_levels++;
@@ -2300,15 +2343,30 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue) {
+            // leaf skip: a pull level's discoveries at ids >= leaf_lo have one neighbour, their parent, so
+            // they sweep nothing; the queue holds the nf_core others (the pull kernel counted them)
+            const bool skip = opt.leaf_skip && nf_core >= 0 && ws->leaf_lo < nv;
+            const int64_t lim = skip ? ws->leaf_lo : nwords * 64;
+            const int64_t cw = (lim + 63) / 64; // words holding ids below lim
             BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
             const int64_t per_block_min = (int64_t)kBS * kCompactWords;
-            const unsigned gb = clamp_grid((nwords + per_block_min - 1) / per_block_min, 256);
-            const int64_t wpb = ((nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
-            hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, nwords, wpb, ws->qa,
-                               ws->d_cursor);
+            const unsigned gb = clamp_grid(std::max<int64_t>((cw + per_block_min - 1) / per_block_min, 1), 256);
+            const int64_t wpb = ((cw + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
+            hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, cw, wpb, ws->qa,
+                               ws->d_cursor, lim);
             BFSX_HIP_TRY(hipGetLastError());
+            if (skip) nf = nf_core;
+            static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
+            if (trace) {
+                u64 qn = 0;
+                BFSX_HIP_TRY(hipMemcpyAsync(&qn, ws->d_cursor, sizeof(qn), hipMemcpyDeviceToHost, st));
+                BFSX_HIP_TRY(hipStreamSynchronize(st));
+                fprintf(stderr, "[bfsx] level %d: bitmap -> queue %llu ids below %lld, nf %lld (skip %d)\n", level,
+                        (unsigned long long)qn, (long long)lim, (long long)nf, (int)skip);
+            }
             in_queue = true;
         }
+        nf_core = -1;
         snapped = false;
         if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(ctx, ws, nf, dmax)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
@@ -2399,6 +2457,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             std::swap(ws->qa, ws->qb);
         } else {
             mu = s.mu; // exact: degree sum of the candidates this level left unvisited
+            nf_core = s.mf; // the single-GPU bottom-up step counts its discoveries below leaf_lo here
             mf = -1;   // not accumulated by the single-GPU bottom-up step
             dmax = -1;
             mfh = -1;
@@ -2600,7 +2659,7 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
         const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
         const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
         hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
-                           ws->d_cursor);
+                           ws->d_cursor, ws->nwords * 64);
         BFSX_HIP_TRY(hipGetLastError());
         ws->d_in_queue = true;
     }
@@ -2763,6 +2822,71 @@ int grow(u64 *&buf, int64_t &cap, int64_t need) {
     return BFSX_OK;
 }
 
+// Once per graph (collective): the ORIGINAL ids of degree > big_degree with their degrees, all-gathered into
+// a sorted host list (u64 id << 32 | degree).  It replaces a table of every id's degree (4 B per id: 4 GiB
+// per rank at scale 30); a Kronecker graph has few such ids (options big_degree = 4096 and big_cap = 2^20
+// ids per rank, else the list overflows and source degrees stay unknown).
+int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
+    hipStream_t st = g->ctx->stream;
+    const int64_t thr = g->ctx->opt.big_degree;
+    const u64 cap = (u64)g->ctx->opt.big_cap;
+    const int P = g->nranks;
+    uint32_t *slice = nullptr;
+    u64 *sel = nullptr, *cnt = nullptr, *all = nullptr;
+    int e = BFSX_OK;
+    std::vector<u64> counts(P, 0);
+    u64 mine = 0, maxc = 0;
+    bool over = false;
+    auto hip_ok = [&](hipError_t r, const char *what) {
+        if (r != hipSuccess && !e) e = fail(BFSX_E_HIP, std::string(what) + ": " + hipGetErrorString(r));
+        return !e;
+    };
+    if (!hip_ok(hipMalloc(&slice, g->chunk * sizeof(uint32_t)), "big list slice") ||
+        !hip_ok(hipMalloc(&sel, cap * sizeof(u64)), "big list") ||
+        !hip_ok(hipMalloc(&cnt, (1 + kMaxRanks) * sizeof(u64)), "big list counts") ||
+        !hip_ok(hipMemsetAsync(cnt, 0, sizeof(u64), st), "big list count"))
+        goto done;
+    hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                       g->d_row_off, g->d_perm, g->nv, g->chunk, slice);
+    hipLaunchKernelGGL(k_select_big, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, slice,
+                       g->chunk, (uint32_t)thr, g->v_lo, sel, cap, cnt);
+    if (!hip_ok(hipGetLastError(), "big list kernels")) goto done;
+    if ((e = cm->allgather(cnt, 1, cnt + 1, st))) goto done;
+    if (!hip_ok(hipMemcpyAsync(counts.data(), cnt + 1, P * sizeof(u64), hipMemcpyDeviceToHost, st), "big list counts") ||
+        !hip_ok(hipStreamSynchronize(st), "big list counts"))
+        goto done;
+    mine = counts[g->rank];
+    if (std::getenv("BFSX_TRACE"))
+        fprintf(stderr, "[bfsx] rank %d: %llu ids of degree > %lld\n", g->rank, (unsigned long long)mine, (long long)thr);
+    for (int p = 0; p < P; p++) {
+        maxc = std::max(maxc, counts[p]);
+        over = over || counts[p] > cap;
+    }
+    ws->h_big.clear();
+    ws->big_overflow = over;
+    if (!over) {
+        maxc = std::max<u64>(maxc, 1);
+        if (!hip_ok(hipMalloc(&all, P * maxc * sizeof(u64)), "big list gather") ||
+            !hip_ok(hipMemsetAsync(sel + mine, 0xFF, (maxc - mine) * sizeof(u64), st), "big list pad"))
+            goto done;
+        if ((e = cm->allgather(sel, (int64_t)maxc, all, st))) goto done;
+        std::vector<u64> h(P * maxc);
+        if (!hip_ok(hipMemcpyAsync(h.data(), all, h.size() * sizeof(u64), hipMemcpyDeviceToHost, st), "big list copy") ||
+            !hip_ok(hipStreamSynchronize(st), "big list copy"))
+            goto done;
+        for (u64 x : h)
+            if (x != ~0ull) ws->h_big.push_back(x);
+        std::sort(ws->h_big.begin(), ws->h_big.end());
+    }
+    ws->big_thr = thr;
+done:
+    (void)hipFree(slice);
+    (void)hipFree(sel);
+    (void)hipFree(cnt);
+    (void)hipFree(all);
+    return e;
+}
+
 // level close: local sums + all-reduce of (n_f, m_f, m_u); returns [0..4] local, [8..10] global
 int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) {
     hipStream_t st = g->ctx->stream;
@@ -2801,44 +2925,38 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
         ws->nnz_global = h[0];
     }
-    if (ws->h_gdeg.empty()) {
-        // once per graph (collective): every rank's slice degrees, all-gathered into a host table, so a
-        // BFS learns its source's global degree (the first level's m_f) with no collective or host wait
-        const int64_t ng = g->chunk * P;
-        u64 *slice = nullptr, *all = nullptr;
-        BFSX_HIP_TRY(hipMalloc(&slice, g->chunk * sizeof(uint32_t)));
-        BFSX_HIP_TRY(hipMalloc(&all, ng * sizeof(uint32_t)));
-        hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                           g->d_row_off, g->d_perm, g->nv, g->chunk, reinterpret_cast<uint32_t *>(slice));
-        int e = hipGetLastError() == hipSuccess ? cm->allgather(slice, g->chunk / 2, all, st) : BFSX_E_HIP;
-        if (!e) {
-            ws->h_gdeg.resize(ng);
-            if (hipMemcpyAsync(ws->h_gdeg.data(), all, ng * sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess)
-                e = fail(BFSX_E_HIP, "degree table copy");
-        }
-        (void)hipFree(slice);
-        (void)hipFree(all);
-        if (e) {
-            ws->h_gdeg.clear();
-            return e;
-        }
+    if (ws->big_thr < 0) {
+        if (int e = dist_big_list(g, ws, cm)) return e; // once per graph (collective)
     }
     if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
-    const int64_t deg = ws->h_gdeg[source]; // original ids index the padded slices directly (v_lo = rank * chunk)
+    // The first level's global m_f is the source's degree, which only its owner holds.  Every rank looks
+    // the source up in the all-gathered list of ids with degree > big_thr: a listed source's degree is
+    // exact; any other source has degree <= big_thr, a bound that sizes the level's fixed exchange slots
+    // just as well (no rank sends more pairs than the source has edges).  An overflowed list leaves the
+    // degree unknown: the level takes the counted exchange.  Decided identically on every rank.
+    int64_t deg = -1, mf = 0;
+    if (!ws->big_overflow) {
+        const auto it = std::lower_bound(ws->h_big.begin(), ws->h_big.end(), (u64)source << 32);
+        if (it != ws->h_big.end() && (int64_t)(*it >> 32) == source) deg = (int64_t)(*it & 0xFFFFFFFFull);
+        mf = deg >= 0 ? deg : ws->big_thr;
+    } else {
+        mf = opt.slot_pairs + 1;
+    }
     int64_t deg_local = 0;
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st)); // before the timed region
     if ((rc = dist_begin(g, source, &deg_local, deg))) return rc;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     const bool owner = source >= g->v_lo && source < g->v_lo + g->nv;
-    int64_t nf = 1, prev_nf = 0, mf = deg, mu = ws->nnz_global - deg, examined = 0;
+    // m_u: an unlisted source's degree (<= big_thr of ~10^9 entries) is left in it until the first pull
+    // level recounts m_u exactly; it only feeds Beamer's switch
+    int64_t nf = 1, prev_nf = 0, mu = ws->nnz_global - std::max<int64_t>(deg, 0), examined = 0;
     // m_u of this rank's unvisited rows.  A pull level reports the exact m_u it leaves (the degree sum
     // of its unvisited candidates), so the m_f of the frontier it found is the m_u it consumed: no
     // per-discovery degree read in the pull kernel.  Before the first pull level the count still holds
     // the isolated self-loop-only rows' entries, which can only over-state that m_f (a safe bound for
     // the next push level's pair buffers).
-    int64_t mu_local = g->nnz - (owner ? deg : 0);
+    int64_t mu_local = g->nnz - (owner ? deg_local : 0);
     int64_t visited_local = owner ? 1 : 0;
     bool snapped = false; // ws->front holds the visited slice from before the last (top-down) level
     int td_levels = 0, bu_levels = 0;
@@ -2869,7 +2987,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
                 const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
                 hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
-                                   ws->d_cursor);
+                                   ws->d_cursor, ws->nwords * 64);
                 BFSX_HIP_TRY(hipGetLastError());
                 ws->d_in_queue = true;
             }
@@ -2958,6 +3076,10 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             bu_levels++;
         }
         if (int e = dist_level_close(g, ws, td, h)) return e;
+        static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
+        if (trace)
+            fprintf(stderr, "[bfsx] rank %d level %d %s: nf %lld -> %lld (global %lld)\n", g->rank, level,
+                    td ? "push" : "pull", (long long)ws->d_nf, (long long)h[0], (long long)h[8]);
         // per-level record (local counts) and state advance
         bfsx_level_stat ls{};
         ls.direction = dir;

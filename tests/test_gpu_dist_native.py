@@ -234,17 +234,26 @@ def test_native_group_hub_domain(bfsx, world, bits):
         check(nv, u, v, sources, out)
 
 
-def test_native_group_source_degrees(bfsx):
-    """The partitioned loop reads a BFS's source degree from its host degree table (every id's degree,
-    all-gathered once per graph): sources of degree 0, in the last rank's partly padded slice, and of
-    the largest degree all give the oracle's distances; an id outside the graph fails on every rank."""
+@pytest.mark.parametrize("options", [{}, {"big_degree": "8"}, {"big_degree": "8", "big_cap": "16"},
+                                     {"big_degree": "0", "slot_pairs": "4"}])
+def test_native_group_source_degrees(bfsx, options):
+    """The partitioned loop's first level needs the source's global degree, which only its owner holds:
+    every rank looks it up in the list of ids with degree > big_degree (all-gathered once per graph, at
+    most big_cap per rank); an unlisted source's degree is bounded by big_degree (fixed exchange slots of
+    that size), an overflowed list leaves it unknown (counted exchange).  Sources of degree 0, in the last
+    rank's partly padded slice, a 5,000-neighbour hub (listed by default) and ordinary ones all give the
+    oracle's distances in every mode; an id outside the graph fails on every rank."""
     rng = np.random.default_rng(31)
     nv = 5003  # not a multiple of 64 * world: the last slice is padded
     u = rng.integers(0, nv - 40, 4 * nv).astype(np.uint32)  # the last 40 ids are isolated
     v = rng.integers(0, nv - 40, 4 * nv).astype(np.uint32)
+    hub = 4000  # degree > 4096 (the default big_degree): a star over every other non-isolated id
+    u = np.r_[u, np.full(nv - 41, hub)].astype(np.uint32)
+    v = np.r_[v, np.delete(np.arange(nv - 40), hub)].astype(np.uint32)
     deg = np.bincount(np.concatenate([u, v]), minlength=nv)
-    sources = [nv - 1, nv - 41, int(np.argmax(deg)), 0]
-    out = run_group(bfsx, 3, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources)
+    assert deg[hub] > 4096
+    sources = [nv - 1, nv - 41, hub, int(np.argmin(np.where(deg > 0, deg, 1 << 30))), 0]
+    out = run_group(bfsx, 3, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, options=options)
     check(nv, u, v, sources, out)
     assert out[0][0]["levels"] == 1 and out[0][0]["reached"] == 1
     ctxs = [bfsx.Context(0) for _ in range(2)]

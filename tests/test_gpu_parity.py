@@ -557,3 +557,61 @@ def test_degree_one_vertices(ctx, direction):
                     check_against_oracle(g, n, off, col, s, u, v, mr=False)
     finally:
         ctx.set_option("direction", "auto")
+
+
+def test_leaf_skip(ctx):
+    """Leaf skip (single device): a pull level's discoveries at ids >= leaf_lo (rows of one entry: the
+    relabelled graph's degree-1 tail) stay out of the next push level's queue -- their one neighbour is
+    their parent.  The pull kernel counts the others, so every later consumer of the queue (k_td, K3p,
+    a hybrid level's queue -> bitmap) sees the shortened length; round 1's leaf filter faulted because
+    consumers kept the unfiltered count.  Distances, pass counts and parents against the oracle, with the
+    option on and off, on (a) a graph whose pull level hands a push level a frontier of leaves only
+    (the push level's queue is empty and the pass still counts), (b) Kronecker graphs over many roots,
+    with and without K3p and hybrid levels."""
+    # (a) s - h - c_i (3,000) ; c_i - leaf_i for i < 1,000 ; 100,000 isolated ids (n/24 above 3,000)
+    s, h = 0, 1
+    c = 2 + np.arange(3000)
+    lv = 3002 + np.arange(1000)
+    u = np.r_[[s], np.full(3000, h), c[:1000]].astype(np.uint32)
+    v = np.r_[[h], c, lv].astype(np.uint32)
+    nv = 4002 + 100000
+    off, col = O.build_sets(nv, u, v)
+    try:
+        for skip in ("on", "off"):
+            ctx.set_option("leaf_skip", skip)
+            with ctx.from_edges(nv, u, v) as g:
+                _, _, st = check_against_oracle(g, nv, off, col, s, u, v, mr=False)
+                assert st["levels"] == 4
+                ls = g.level_stats()
+                assert [x["direction"] for x in ls] == [1, 2, 2, 1], ls
+                if skip == "on":
+                    assert ls[3]["frontier_in"] == 0  # the leaves stayed out of the queue
+                else:
+                    assert ls[3]["frontier_in"] == 1000
+        # (b) Kronecker: identical results with and without the skip, across K3p / hybrid settings
+        ou, ov = O.kronecker(16, 16, 0x1EAF)
+        nv = 1 << 16
+        off, col = O.build_sets(nv, ou, ov)
+        shortened = 0
+        for persist, hybrid in (("on", "auto"), ("off", "auto"), ("on", "force")):
+            ctx.set_option("persist", persist)
+            ctx.set_option("hybrid", hybrid)
+            res = {}
+            for skip in ("off", "on"):
+                ctx.set_option("leaf_skip", skip)
+                with ctx.kronecker(16, 16, 0x1EAF) as g:
+                    roots = [int(r) for r in g.sample_roots(12, seed=5)]
+                    for r in roots:
+                        d, p, st = g.bfs(r)
+                        res.setdefault(r, []).append((d, st["levels"], g.level_stats()))
+                        assert O.validate(nv, off, col, r, d, p) == 0
+            for r, ((d0, l0, s0), (d1, l1, s1)) in res.items():
+                assert np.array_equal(d0, d1) and l0 == l1
+                shortened += sum(1 for a, b in zip(s0, s1) if b["frontier_in"] < a["frontier_in"])
+            ref, _ = O.csr_bfs(nv, off, col, roots[0])
+            assert np.array_equal(res[roots[0]][0][0], ref)
+        assert shortened > 0  # the skip applied somewhere
+    finally:
+        ctx.set_option("persist", "on")
+        ctx.set_option("hybrid", "auto")
+        ctx.set_option("leaf_skip", "on")
