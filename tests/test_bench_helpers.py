@@ -73,3 +73,25 @@ def test_measured_traffic_requires_matching_source(bench, tmp_path, monkeypatch)
     rec["kernels_bfs_sha"] = "0" * 16
     (prof / "zz_hbm.json").write_text(json.dumps(rec))
     assert bench.measured_traffic()["traffic"] is None
+
+
+def test_pick_roots_skips_tiny_components(bench):
+    """Roots in components of under 1/1000 of the tuples are skipped (and listed); the rest keep the
+    sampling order; a graph without tiny components keeps exactly the first roots."""
+    class G:
+        def sample_roots(self, n, seed):
+            return list(range(100, 100 + n))
+
+    class A:
+        roots, root_seed = 5, 1
+
+    m = 10_000
+    small = {101: 3, 104: 9}
+    calls = []
+    roots, mcomp, errors, skipped = bench.pick_roots(
+        A, G(), m, lambda r: small.get(r, 9_000), lambda: calls.append(1) or 0)
+    assert roots == [100, 102, 103, 105, 106]
+    assert skipped == [{"root": 101, "m_comp": 3}, {"root": 104, "m_comp": 9}]
+    assert errors == 0 and len(calls) == 5 and mcomp[100] == 9_000
+    roots, _, _, skipped = bench.pick_roots(A, G(), m, lambda r: 10, lambda: 0)
+    assert roots == [100, 101, 102, 103, 104] and skipped == []
