@@ -2831,60 +2831,65 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
     const int64_t thr = g->ctx->opt.big_degree;
     const u64 cap = (u64)g->ctx->opt.big_cap;
     const int P = g->nranks;
-    uint32_t *slice = nullptr;
-    u64 *sel = nullptr, *cnt = nullptr, *all = nullptr;
-    int e = BFSX_OK;
+    // Collective: every rank takes part in both all-gathers whatever happens locally.  Everything that can
+    // fail on one rank (allocations, the selection kernels) happens before the first one, and a failed rank
+    // posts the count ~0, so that all ranks leave together with the same error.
+    struct Bufs {
+        uint32_t *slice = nullptr;
+        u64 *sel = nullptr, *cnt = nullptr, *all = nullptr;
+        ~Bufs() {
+            for (void *p : {(void *)slice, (void *)sel, (void *)cnt, (void *)all})
+                if (p) (void)hipFree(p);
+        }
+    } b;
+    BFSX_HIP_TRY(hipMalloc(&b.cnt, (1 + kMaxRanks) * sizeof(u64)));
+    bool ok = hipMalloc(&b.slice, g->chunk * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&b.sel, cap * sizeof(u64)) == hipSuccess &&
+              hipMalloc(&b.all, (size_t)P * cap * sizeof(u64)) == hipSuccess &&
+              hipMemsetAsync(b.cnt, 0, sizeof(u64), st) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                           g->d_row_off, g->d_perm, g->nv, g->chunk, b.slice);
+        hipLaunchKernelGGL(k_select_big, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                           b.slice, g->chunk, (uint32_t)thr, g->v_lo, b.sel, cap, b.cnt);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        const u64 bad = ~0ull;
+        BFSX_HIP_TRY(hipMemcpyAsync(b.cnt, &bad, sizeof(bad), hipMemcpyHostToDevice, st));
+    }
+    if (int e = cm->allgather(b.cnt, 1, b.cnt + 1, st)) return e;
     std::vector<u64> counts(P, 0);
-    u64 mine = 0, maxc = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(counts.data(), b.cnt + 1, P * sizeof(u64), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    u64 maxc = 0;
     bool over = false;
-    auto hip_ok = [&](hipError_t r, const char *what) {
-        if (r != hipSuccess && !e) e = fail(BFSX_E_HIP, std::string(what) + ": " + hipGetErrorString(r));
-        return !e;
-    };
-    if (!hip_ok(hipMalloc(&slice, g->chunk * sizeof(uint32_t)), "big list slice") ||
-        !hip_ok(hipMalloc(&sel, cap * sizeof(u64)), "big list") ||
-        !hip_ok(hipMalloc(&cnt, (1 + kMaxRanks) * sizeof(u64)), "big list counts") ||
-        !hip_ok(hipMemsetAsync(cnt, 0, sizeof(u64), st), "big list count"))
-        goto done;
-    hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                       g->d_row_off, g->d_perm, g->nv, g->chunk, slice);
-    hipLaunchKernelGGL(k_select_big, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, slice,
-                       g->chunk, (uint32_t)thr, g->v_lo, sel, cap, cnt);
-    if (!hip_ok(hipGetLastError(), "big list kernels")) goto done;
-    if ((e = cm->allgather(cnt, 1, cnt + 1, st))) goto done;
-    if (!hip_ok(hipMemcpyAsync(counts.data(), cnt + 1, P * sizeof(u64), hipMemcpyDeviceToHost, st), "big list counts") ||
-        !hip_ok(hipStreamSynchronize(st), "big list counts"))
-        goto done;
-    mine = counts[g->rank];
-    if (std::getenv("BFSX_TRACE"))
-        fprintf(stderr, "[bfsx] rank %d: %llu ids of degree > %lld\n", g->rank, (unsigned long long)mine, (long long)thr);
     for (int p = 0; p < P; p++) {
+        if (counts[p] == ~0ull)
+            return fail(BFSX_E_OOM, "degree list of the partitioned loop: rank " + std::to_string(p) +
+                                        " could not allocate or select its ids");
         maxc = std::max(maxc, counts[p]);
         over = over || counts[p] > cap;
     }
+    const u64 mine = counts[g->rank];
+    if (std::getenv("BFSX_TRACE"))
+        fprintf(stderr, "[bfsx] rank %d: %llu ids of degree > %lld\n", g->rank, (unsigned long long)mine, (long long)thr);
     ws->h_big.clear();
     ws->big_overflow = over;
     if (!over) {
         maxc = std::max<u64>(maxc, 1);
-        if (!hip_ok(hipMalloc(&all, P * maxc * sizeof(u64)), "big list gather") ||
-            !hip_ok(hipMemsetAsync(sel + mine, 0xFF, (maxc - mine) * sizeof(u64), st), "big list pad"))
-            goto done;
-        if ((e = cm->allgather(sel, (int64_t)maxc, all, st))) goto done;
+        BFSX_HIP_TRY(hipMemsetAsync(b.sel + mine, 0xFF, (maxc - mine) * sizeof(u64), st));
+        if (int e = cm->allgather(b.sel, (int64_t)maxc, b.all, st)) return e;
         std::vector<u64> h(P * maxc);
-        if (!hip_ok(hipMemcpyAsync(h.data(), all, h.size() * sizeof(u64), hipMemcpyDeviceToHost, st), "big list copy") ||
-            !hip_ok(hipStreamSynchronize(st), "big list copy"))
-            goto done;
+        BFSX_HIP_TRY(hipMemcpyAsync(h.data(), b.all, h.size() * sizeof(u64), hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipStreamSynchronize(st));
         for (u64 x : h)
             if (x != ~0ull) ws->h_big.push_back(x);
         std::sort(ws->h_big.begin(), ws->h_big.end());
     }
     ws->big_thr = thr;
-done:
-    (void)hipFree(slice);
-    (void)hipFree(sel);
-    (void)hipFree(cnt);
-    (void)hipFree(all);
-    return e;
+    return BFSX_OK;
 }
 
 // level close: local sums + all-reduce of (n_f, m_f, m_u); returns [0..4] local, [8..10] global
