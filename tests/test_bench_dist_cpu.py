@@ -1,0 +1,35 @@
+"""bench.py's N > 1 harness at world_size 2 over gloo on the CPU (tests/bench_dist_fake.py stands in for
+the GPU library): one JSON line from rank 0, n_gpus = 2, strong scaling, and `value` = the harmonic mean
+of m_comp over the SLOWEST rank's device time of each BFS, with a tiny-component root skipped."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def test_bench_dist_harness_two_ranks_gloo():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "tests", "bench_dist_fake.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["steps"] == 2
+    assert d["metric"] == "GTEPS (harmonic mean, 4 roots) on RMAT scale-12"
+    roots = [1, 2, 4, 5]  # root 3 skipped: its component holds 5 of 65,536 tuples
+    assert d["validation"]["skipped_tiny_component"] == [{"root": 3, "m_comp": 5}]
+    m_comp = (16 << 12) // 2
+    slowest = [1.0 + 0.5 * 1 + 0.01 * r for r in roots] * 2  # rank 1's times, 2 steps
+    want = len(slowest) / sum(t * 1e-3 * 1e9 / m_comp for t in slowest)
+    assert abs(d["value"] - want) < 1e-9 * want
+    assert d["bfs_runs"] == 8 and d["config"]["parallelism"].startswith("1d-partition dp2")
