@@ -118,7 +118,12 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 total exchanges its pairs through fixed per-peer slots, skipping the count all-to-all
  *                 and its host wait; default 16384, 0 = never)
  *   "build_chunk" = int (CSR build: raw adjacency entries per sort/dedup chunk, default 2^30; bounds the
- *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device) */
+ *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device)
+ *   "leaf_skip" = on|off (single device: the degree-1 vertices a pull level discovers stay out of the next
+ *                 push level's queue -- their one neighbour is their parent; default on)
+ *   "big_degree", "big_cap" = int (partitioned graphs: the ids of degree > big_degree, at most big_cap per
+ *                 rank, are all-gathered with their degrees at the first BFS, so every rank knows a source's
+ *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */
