@@ -1143,7 +1143,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
-    __shared__ uint32_t s_miss[kWaves][(64 * kU)];
+    // phase B's rows; the hub sweep (kHubOnly) carries them over rounds until a full 64-lane batch is ready
+    __shared__ uint32_t s_miss[kWaves][(64 * kU) + (kHubOnly ? 64 : 0)];
     __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
     // the frontier bits of the first pf.ids ids of every id range (the highest-degree vertices of a
     // relabelled graph, where most probes land) copied to LDS once per workgroup; pf.ids = 0: off
@@ -1210,6 +1211,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                     xn[k] = (hb + (uint32_t)k * 64 + lane < he) ? top1[vk] : 0u;
                 }
             }
+            uint32_t nmiss = 0; // wave-uniform: phase-B rows waiting in s_miss
             for (uint32_t t0 = hb; t0 < he; t0 += (64 * kU)) {
                 uint32_t v[kU], x[kU];
 #pragma unroll
@@ -1260,7 +1262,6 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                     if (r[k].w != 0u)
                         pbm |= (fbit(r[k].x) | (fbit(r[k].y) << 1) | (fbit(r[k].z) << 2)) << (3 * k);
                 }
-                uint32_t nmiss = 0; // wave-uniform
 #pragma unroll
                 for (int k = 0; k < kU; k++) {
                     const bool ok = t0 + (uint32_t)k * 64 + lane < he;
@@ -1306,9 +1307,13 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                     nmiss += (uint32_t)__popcll(mm);
                 }
                 __builtin_amdgcn_wave_barrier();
-                // B: rows longer than 4 with no hit in their first 4 entries walk the rest, 8 per step
-                for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
-                    if (m0 + lane < nmiss) {
+                // B: rows longer than 4 with no hit in their first 4 entries walk the rest, 8 per step.  The
+                // hub sweep walks them in full 64-row batches only (fewer rows wait for the next round, the
+                // half's last round walks the rest): hybrid levels 599 -> 546 us.  The pull levels do not
+                // gain from it and their sparse levels lose (profiles/r02r/deferred_phaseB_ab.txt).
+                const uint32_t nb = (!kHubOnly || t0 + 64 * kU >= he) ? nmiss : (nmiss & ~63u); // wave-uniform
+                for (uint32_t m0 = 0; m0 < nb; m0 += 64) {
+                    if (m0 + lane < nb) {
                         const uint32_t vv = s_miss[wave][m0 + lane];
                         const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
                         bool found = false, stop = false;
@@ -1358,6 +1363,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
                         }
                     }
                 }
+                if (kHubOnly && nb && nb < nmiss && lane < nmiss - nb) // carry the < 64 left to the front
+                    s_miss[wave][lane] = s_miss[wave][nb + lane];
+                nmiss -= nb;
                 __builtin_amdgcn_wave_barrier();
             }
             __builtin_amdgcn_wave_barrier(); // the next half rewrites the list
