@@ -18,6 +18,9 @@ K x 64 timed BFS runs.
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu-baseline]
+
+--gpus N > 1 without a launcher (WORLD_SIZE unset) starts the N ranks itself, as one child
+`python -m torch.distributed.run --nproc-per-node N` process, and relays its JSON line (launch_ranks).
 """
 import argparse
 import importlib.util
@@ -34,7 +37,11 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def load_module(name, file):
-    spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, file))
+    # test hook: BFSX_BENCH_BINDING names a stand-in for the libbfsx binding (tests/bench_dist_fake.py),
+    # so the launcher and the N > 1 harness run on a CPU-only box
+    override = os.environ.get("BFSX_BENCH_BINDING")
+    path = override if override and name == "bfsx" else os.path.join(PKG, file)
+    spec = importlib.util.spec_from_file_location(name, path)
     mod = importlib.util.module_from_spec(spec)
     sys.modules[name] = mod
     spec.loader.exec_module(mod)
@@ -79,6 +86,9 @@ def parse_args():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--serial-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the OpenMP CPU baseline (default: the box's CPU share, OMP_NUM_THREADS, "
+                         "else the affinity mask)")
     ap.add_argument("--no-p1", action="store_true", help="skip the partitioned-path P=1 rehearsal at N=1")
     ap.add_argument("--direction", default="auto")
     ap.add_argument("--levels-json", default="")
@@ -241,8 +251,11 @@ def cpu_baselines(args, g, roots, mcomp, nv):
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = nproc
+    # The GPU box gives one GPU's job a CPU share of 16 threads (OMP_NUM_THREADS=16 there, which jobs
+    # must leave alone) while os.cpu_count() / the affinity mask show the whole host; the row runs on that
+    # share and says so.  --cpu-threads overrides it.
     env_threads = int(os.environ.get("OMP_NUM_THREADS", "0"))
-    nthreads = env_threads or affinity
+    nthreads = args.cpu_threads or env_threads or affinity
     off, col = g.csr()
     samples, spent = [], 0.0
     for r in roots:
@@ -261,7 +274,8 @@ def cpu_baselines(args, g, roots, mcomp, nv):
         "cores": nthreads,
         "nproc": nproc,
         "affinity_cpus": affinity,
-        "threads_from": "OMP_NUM_THREADS" if env_threads else "sched_getaffinity",
+        "threads_from": ("--cpu-threads" if args.cpu_threads else
+                         "OMP_NUM_THREADS (the job's CPU share on the GPU box)" if env_threads else "sched_getaffinity"),
         "kind": "port",
         "sample": f"{len(samples)} root(s) of the same scale-{args.scale} graph, oracle orc_mapreduce_bfs "
                   f"(BfsSpark map/reduce restated, OpenMP), {spent:.1f} s; distances asserted equal to the GPU's",
@@ -361,6 +375,15 @@ def run_single(args):
     wall = time.perf_counter() - w0
 
     gteps = [mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(order, t_bfs)]
+    # output conversion (outside t_bfs): the unpack kernel that turns the packed internal-id state into the
+    # original-id int32 dist / parent arrays the C-ABI promises, then the PCIe copy of dist + int64 parent
+    unpack_ms, d2h_ms = [], []
+    for r in roots[:4]:
+        g.bfs_device_only(r)
+        c0 = time.perf_counter()
+        g.result(want_parent=True)
+        d2h_ms.append((time.perf_counter() - c0) * 1e3)
+        unpack_ms.append(g.last_unpack_ms())
     cpu = serial = None
     if not args.no_cpu_baseline and args.cpu_baseline_seconds > 0 and g.nnz < (1 << 32):
         cpu, serial = cpu_baselines(args, g, roots, mcomp, nv)
@@ -373,6 +396,11 @@ def run_single(args):
     out["whole_bfs_roofline"] = acct.whole(float(np.sum(t_bfs)), len(t_bfs))
     out["edge_scan_equivalent"] = edge_scan_equivalent(g.m, nv, float(np.mean(t_bfs)))
     out.update({"t_bfs_ms_mean": float(np.mean(t_bfs)), "t_bfs_ms_min": float(np.min(t_bfs)),
+                "t_unpack_ms": round(float(np.mean(unpack_ms)), 4),
+                "t_result_copy_ms": round(float(np.mean(d2h_ms)), 3),
+                "output_note": "t_unpack_ms: device time of the unpack kernel (internal-id packed state -> "
+                               "original-id int32 dist + parent), outside t_bfs; t_result_copy_ms: host wall "
+                               "time of bfsx_result (unpack + D2H of dist and int64 parent), 4 roots",
                 "bfs_runs": len(t_bfs), "m_comp_mean": float(np.mean([mcomp[r] for r in order])),
                 "graph_build_s": round(build_s, 3),
                 "validation": {"roots": len(roots), "errors": val_errors, "skipped_tiny_component": skipped,
@@ -493,9 +521,43 @@ def run_dist(args, world, rank, local_rank):
         print(json.dumps(out), flush=True)
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) run without a launcher -- how the driver calls it: start N ranks as ONE child
+    process, `python -m torch.distributed.run --nproc-per-node N ... bench.py <the same arguments>`, before
+    this process touches HIP or torch, relay the child's single JSON line to stdout and return its exit
+    code.  Everything else the child prints goes to stderr."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] --gpus {args.gpus}: launching {' '.join(cmd)}", file=sys.stderr, flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    js = [ln for ln in lines if ln.lstrip().startswith("{")]
+    for ln in lines:
+        if ln not in js:
+            print(ln, file=sys.stderr)
+    if r.returncode != 0 or len(js) != 1:
+        print(f"[bench] ranks exited {r.returncode} with {len(js)} JSON line(s)", file=sys.stderr, flush=True)
+        return r.returncode or 1
+    print(js[0], flush=True)
+    return 0
+
+
 def main():
     args = parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus and not (world == 1 and args.dist):
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a different GPU count",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1 or args.dist:
         run_dist(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
     else:

@@ -36,9 +36,14 @@ EXPORTS = [
     "bfsx_result", "bfsx_level_times", "bfsx_level_dirs", "bfsx_level_stats",
     "bfsx_device_synchronize", "bfsx_validate", "bfsx_validate_result",
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
+    "bfsx_last_bfs_ms", "bfsx_last_unpack_ms", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group",
+    "bfsx_dist_bfs",
+]
+# test-only level primitives (include/bfsx_levels.h): exported for tests/dist_driver.py, not product ABI
+TEST_EXPORTS = [
     "bfsx_dist_begin", "bfsx_dist_frontier_info", "bfsx_dist_td_expand", "bfsx_dist_td_claim",
     "bfsx_dist_frontier_slice", "bfsx_dist_bu_step", "bfsx_dist_level_end", "bfsx_dist_finish",
-    "bfsx_dist_mcomp", "bfsx_last_bfs_ms", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group", "bfsx_dist_bfs",
+    "bfsx_dist_mcomp",
 ]
 COMM_ID_BYTES = 128
 
@@ -106,6 +111,7 @@ def lib():
         L.bfsx_level_times.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_last_bfs_ms.argtypes = [_VP, C.POINTER(C.c_double)]
+        L.bfsx_last_unpack_ms.argtypes = [_VP, C.POINTER(C.c_double)]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
         L.bfsx_device_synchronize.argtypes = [_VP]
         I64P = C.POINTER(C.c_int64)
@@ -304,6 +310,13 @@ class Graph:
         """Device time (ms) of the most recent BFS of this graph (bfsx_last_bfs_ms)."""
         ms = C.c_double()
         _check(lib().bfsx_last_bfs_ms(self._h, C.byref(ms)))
+        return ms.value
+
+    def last_unpack_ms(self):
+        """Device time (ms) of the unpack kernel of the most recent result copy (bfsx_last_unpack_ms): the
+        packed internal-id state -> original-id dist / parent arrays, outside t_bfs; -1 if none ran."""
+        ms = C.c_double()
+        _check(lib().bfsx_last_unpack_ms(self._h, C.byref(ms)))
         return ms.value
 
     def result(self, want_parent=True):

@@ -1,4 +1,5 @@
-// bfsx_api.cpp -- the C-ABI of libbfsx.so (declared in include/bfsx.h).
+// bfsx_api.cpp -- the C-ABI of libbfsx.so (declared in include/bfsx.h; the test-only level primitives in
+// include/bfsx_levels.h).
 //
 // Host side of the drop-in boundary: error plumbing, the algs4 edge-list parser with
 // GraphFileUtil.convert semantics (GraphFileUtil.java:45-66), graph handles, root sampling and the
@@ -15,6 +16,7 @@
 #include <string>
 #include <unordered_set>
 
+#include "../../include/bfsx_levels.h"
 #include "bfsx_internal.h"
 #include "java_digits.h"
 
@@ -316,6 +318,29 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         const long long x = strtoll(value, &end, 10);
         if (!end || *end || x < 0) return fail(BFSX_E_ARG, "slot_pairs must be a pair count >= 0");
         ctx->opt.slot_pairs = x;
+        return BFSX_OK;
+    }
+    if (k == "poison_queues") {
+        if (v == "on") ctx->opt.poison_queues = true;
+        else if (v == "off") ctx->opt.poison_queues = false;
+        else return fail(BFSX_E_ARG, "poison_queues must be on|off");
+        return BFSX_OK;
+    }
+    if (k == "bu_force_spill") {
+        if (v == "on") ctx->opt.bu_force_spill = true;
+        else if (v == "off") ctx->opt.bu_force_spill = false;
+        else return fail(BFSX_E_ARG, "bu_force_spill must be on|off");
+        return BFSX_OK;
+    }
+    if (k == "test_overread") {
+        if (v == "off") {
+            ctx->opt.test_overread = -1;
+            return BFSX_OK;
+        }
+        char *end = nullptr;
+        const long x = strtol(value, &end, 10);
+        if (!end || *end || x < 0 || x > (1L << 20)) return fail(BFSX_E_ARG, "test_overread must be off|level >= 0");
+        ctx->opt.test_overread = (int)x;
         return BFSX_OK;
     }
     if (k == "leaf_skip") {
@@ -748,7 +773,7 @@ int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
 
 int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
-    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: drive it with bfsx_dist_* (bfsx_dist.py)");
+    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: run it with bfsx_dist_bfs (collective over the ranks)");
     const auto t0 = std::chrono::steady_clock::now();
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     if (source < 0 || source >= g->nv)
@@ -852,6 +877,12 @@ int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms) {
     if (!g || !ms) return fail(BFSX_E_ARG, "bad argument");
     if (g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
     *ms = g->last_t_bfs_ms;
+    return BFSX_OK;
+}
+
+int bfsx_last_unpack_ms(const bfsx_graph *g, double *ms) {
+    if (!g || !ms) return fail(BFSX_E_ARG, "bad argument");
+    *ms = bfs_last_unpack_ms(g);
     return BFSX_OK;
 }
 

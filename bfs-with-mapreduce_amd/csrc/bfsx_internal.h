@@ -49,6 +49,9 @@ struct Options {
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
     int persist_abort_at = -1;  // test hook: K3p aborts at this level of its launch (-1: never)
     int64_t persist_dmax = 2048; // K3p only while every frontier vertex has at most this degree
+    bool poison_queues = false; // test hook: fill the frontier queues and hub list with 0xFF before every BFS
+    bool bu_force_spill = false; // diagnostic: the partitioned pull kernel in a spilling (8 waves/SIMD) build
+    int test_overread = -1;     // test hook: that top-down level's kernels read one queue entry past the tail
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------
@@ -100,6 +103,8 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
 int64_t bfs_persist_fallbacks(const bfsx_graph *g); // BFS runs re-run without K3p after a barrier abort
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
+// device time (ms) of the most recent copy's unpack kernel (packed state -> original-id dist/parent); -1: none
+double bfs_last_unpack_ms(const bfsx_graph *g);
 // multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
 int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue);

@@ -111,6 +111,14 @@ struct BfsWorkspace {
     uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
     u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
+    // result staging of bfsx_bfs / bfsx_result (int32 dist, int32 parent in original ids): its own
+    // buffers, allocated at the first copy -- never the frontier queues, whose stale words must not be
+    // result data and whose result data must not be frontier ids
+    int32_t *out_dist = nullptr, *out_par = nullptr;
+    hipEvent_t ev_unpack0 = nullptr, ev_unpack1 = nullptr;
+    double last_unpack_ms = -1.0;       // device time of the most recent unpack (state -> original-id arrays)
+    // mapped pinned word: 0, or 1 << 32 | id of the first out-of-range id a queue consumer met (id_ok)
+    u64 *h_err = nullptr, *d_err = nullptr;
     LevelSlot *ring = nullptr;          // device, 3 slots
     LevelSlot *h_slot = nullptr;        // pinned host mirror of one slot
     Published *h_pub = nullptr, *d_pub = nullptr; // mapped pinned level counters (host / device view)
@@ -378,10 +386,22 @@ struct Part {
     uint32_t lo;     // first owned global id
     uint32_t chunk;  // ids per rank (multiple of 64)
     uint32_t rank;
-    uint32_t pad;
+    uint32_t nrows;  // rows held here: every queued id must be below it (id_ok)
     u64 *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
     u64 *remote_tail; // their allocation cursor
+    u64 *err;         // mapped host word: set when a queue holds an id >= nrows (null: unchecked)
 };
+
+// Queue-entry guard.  Every kernel that reads vertex ids out of a frontier queue, the hub list or an
+// exchange buffer checks them against the rows it holds before using them as an index: a stale or
+// poisoned entry (a consumer reading past a queue's tail) is reported to the host (bfs_run fails with
+// BFSX_E_HIP) and skipped, instead of becoming a wild row_off / col / state access.  One compare per
+// frontier vertex; the store happens only on a bad id.
+__device__ inline bool id_ok(uint32_t u, uint32_t nrows, u64 *err) {
+    if (u < nrows) return true;
+    if (err) *reinterpret_cast<volatile u64 *>(err) = 0x100000000ull | u;
+    return false;
+}
 
 // Remote pairs, LDS-buffered like the local queue (multi-GPU path only).
 constexpr int kRCap = 1024;
@@ -498,7 +518,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
         const uint32_t i = base + tid;
         uint32_t deg = 0, u = 0;
         int64_t beg = 0;
-        if ((int)tid < gsz && i < qlen) {
+        if ((int)tid < gsz && i < qlen && id_ok(qin[i], pt.nrows, pt.err)) {
             u = qin[i];
             beg = (int64_t)row_off[u];
             int64_t d = (int64_t)row_off[u + 1] - beg;
@@ -575,10 +595,11 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
             d[k] = 0;
             if (idx < hb) {
                 const uint32_t u = hubs[h0 + idx];
-                const int64_t b = (int64_t)row_off[u];
-                d[k] = (u64)((int64_t)row_off[u + 1] - b);
+                const bool ok = id_ok(u, pt.nrows, pt.err);
+                const int64_t b = ok ? (int64_t)row_off[u] : 0;
+                d[k] = ok ? (u64)((int64_t)row_off[u + 1] - b) : 0ull;
                 s_beg[idx] = b;
-                s_u[idx] = u;
+                s_u[idx] = ok ? u : 0u;
             }
             local += d[k];
         }
@@ -704,7 +725,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
                                                     PersistOut *out, HubSet hs, int64_t bu_floor,
-                                                    int inject_abort, u64 dmax_cap) {
+                                                    int inject_abort, u64 dmax_cap, uint32_t nrows, u64 *err) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_scan[kBS + 1];
@@ -741,6 +762,7 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             if (i < ve) {
                 if (it == 0) {
                     u = q0[i];
+                    if (!id_ok(u, nrows, err)) u = 0xFFFFFFFFu;
                 } else { // segment s of frontier index i: the last with s_off[s] <= i
                     int lo = 0, hi = (int)G - 1;
                     while (lo < hi) {
@@ -750,8 +772,12 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
                     }
                     u = ld_sc1(sin + (size_t)lo * kRegion + (i - s_off[lo]));
                 }
-                beg = (int64_t)row_off[u];
-                deg = (uint32_t)((int64_t)row_off[u + 1] - beg);
+                if (u != 0xFFFFFFFFu) {
+                    beg = (int64_t)row_off[u];
+                    deg = (uint32_t)((int64_t)row_off[u + 1] - beg);
+                } else {
+                    u = 0; // a rejected q0 entry: an empty row
+                }
             }
             const uint32_t inc = wave_incl_scan(deg);
             if (lane == 63) s_wsum[wave] = inc;
@@ -941,7 +967,8 @@ template <class OffT>
 __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pairs, u64 npairs,
                                                       const OffT *__restrict__ row_off, u64 *vis,
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
-                                                      LevelSlot *ring, int level, uint32_t lo, u64 slot) {
+                                                      LevelSlot *ring, int level, uint32_t lo, u64 slot,
+                                                      uint32_t nrows, u64 *err) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ BlockQueue q;
     bq_init(q);
@@ -964,7 +991,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
         if (have) {
             const u64 pr = pairs[at];
             vl = (uint32_t)(pr >> 32) - lo;
-            if (claim(vl, vis, attempts)) {
+            if (id_ok(vl, nrows, err) && claim(vl, vis, attempts)) {
                 win = true;
                 stt[vl] = pack_state((uint32_t)pr, nd);
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
@@ -1132,8 +1159,10 @@ constexpr uint32_t kPrefIds = 1u << 16; // LDS frontier prefix: 8 KiB per workgr
 struct PrefixSpec {
     uint32_t ids, nseg, shift, pad;
 };
-template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+// kSpill: a diagnostic instantiation compiled for 8 waves per SIMD (64 VGPRs), so it spills to scratch --
+// option bu_force_spill, the round-2 "spilling pull kernel + concurrent in-process ranks" experiment.
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe, bool kSpill = false>
+__device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
@@ -1213,6 +1242,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
             }
             uint32_t nmiss = 0; // wave-uniform: phase-B rows waiting in s_miss
             for (uint32_t t0 = hb; t0 < he; t0 += (64 * kU)) {
+                // diagnostic kSpill build: 48 VGPRs clobbered per round leave the live state too few
+                // registers under the 96 of 5 waves/SIMD, so the compiler spills it to scratch
+                if constexpr (kSpill) asm volatile("" ::: "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71");
                 uint32_t v[kU], x[kU];
 #pragma unroll
                 for (int k = 0; k < kU; k++) // past the half's end: masked below
@@ -1381,11 +1413,33 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
     publish_if_last(cn, pub, seq);
 }
 
+#define BFSX_K_BU_PARAMS                                                                                        \
+    const OffT *__restrict__ row_off, const uint32_t *__restrict__ col, const uint32_t *__restrict__ top1,      \
+        const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next,                  \
+        u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level, int64_t nwords, uint32_t fmask, \
+        const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo, \
+        PrefixSpec pf, Published *pub, u64 seq
+#define BFSX_K_BU_ARGS                                                                                          \
+    row_off, col, top1, rest, front, next, vis, stt, ring, level, nwords, fmask, hfront, hub_id, hub_lim, leaf_lo, pf, \
+        pub, seq
+
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu(BFSX_K_BU_PARAMS) {
+    k_bu_body<OffT, kMf, kHubs, kU, kHubOnly, kPipe>(BFSX_K_BU_ARGS);
+}
+// Diagnostic only (option bu_force_spill): the partitioned pipelined pull kernel built so that it
+// spills to scratch -- the round-2 "spilling pull kernel + concurrent in-process ranks" experiment.
+template <class OffT>
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu_spill(BFSX_K_BU_PARAMS) {
+    k_bu_body<OffT, true, false, 4, false, true, true>(BFSX_K_BU_ARGS);
+}
+
 // ---- K4: frontier representation changes -------------------------------------------------------
-__global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restrict__ q, uint32_t qlen, u64 *bm) {
+__global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restrict__ q, uint32_t qlen, u64 *bm,
+                                                         uint32_t nrows, u64 *err) {
     for (uint32_t i = blockIdx.x * kBS + threadIdx.x; i < qlen; i += gridDim.x * kBS) {
         const uint32_t v = q[i];
-        atomicOr(bm + (v >> 6), 1ull << (v & 63u));
+        if (id_ok(v, nrows, err)) atomicOr(bm + (v >> 6), 1ull << (v & 63u));
     }
 }
 
@@ -1393,11 +1447,11 @@ __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restr
 // the queue; its length is known to the host only after the level is published).
 // Publishes the level (hybrid levels end with it).
 __global__ __launch_bounds__(kBS) void k_queue_to_bitmap_dev(const uint32_t *__restrict__ q, LevelSlot *cn, u64 *bm,
-                                                             Published *pub, u64 seq) {
+                                                             Published *pub, u64 seq, uint32_t nrows, u64 *err) {
     const uint32_t n = (uint32_t)cn->qtail;
     for (uint32_t i = blockIdx.x * kBS + threadIdx.x; i < n; i += gridDim.x * kBS) {
         const uint32_t v = q[i];
-        atomicOr(bm + (v >> 6), 1ull << (v & 63u));
+        if (id_ok(v, nrows, err)) atomicOr(bm + (v >> 6), 1ull << (v & 63u));
     }
     publish_if_last(cn, pub, seq);
 }
@@ -1847,6 +1901,9 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipHostMalloc(&ws->h_pub, sizeof(Published), hipHostMallocMapped | hipHostMallocCoherent));
     BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&ws->d_pub, ws->h_pub, 0));
     ws->h_pub->seq = 0;
+    BFSX_HIP_TRY(hipHostMalloc(&ws->h_err, sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent));
+    BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&ws->d_err, ws->h_err, 0));
+    *ws->h_err = 0;
     BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(u64)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
@@ -1883,6 +1940,24 @@ int ws_alloc(bfsx_graph *g) {
     ws->n_dead = (int64_t)nd[0] - (ws->nwords * 64 - g->nv); // minus padding bits
     ws->leaf_lo = (int64_t)nd[1];
     return BFSX_OK;
+}
+
+// The single-device "partition": every row local, queue entries checked against nv (id_ok).
+Part single_part(const bfsx_graph *g, const BfsWorkspace *ws) {
+    Part p{};
+    p.nrows = (uint32_t)g->nv;
+    p.err = ws->d_err;
+    return p;
+}
+
+// After a BFS: fail if a queue consumer met an out-of-range id (the word is cleared for the next BFS).
+int check_queue_guard(BfsWorkspace *ws) {
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const u64 e = *reinterpret_cast<volatile u64 *>(ws->h_err);
+    if (!e) return BFSX_OK;
+    *reinterpret_cast<volatile u64 *>(ws->h_err) = 0;
+    return fail(BFSX_E_HIP, "internal error: a frontier-queue consumer read vertex id " +
+                                std::to_string((uint32_t)e) + ", outside the rows of this graph (stale queue entry)");
 }
 
 // ---- launch helpers: one per traversal kernel, dispatching on the row-offset width -------------
@@ -1950,7 +2025,7 @@ PrefixSpec lds_prefix(const bfsx_graph *g, const BfsWorkspace *ws) {
     return per ? PrefixSpec{per, (uint32_t)g->nranks, (uint32_t)shift, 0u} : off;
 }
 
-template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
+template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe, bool kSpill = false>
 int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
                 u64 seq) {
     hipStream_t st = g->ctx->stream;
@@ -1958,7 +2033,9 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     // leave most CUs idle at the tail of the grid-stride loop)
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>, kBS, 0) !=
+        const void *kfn = kSpill ? reinterpret_cast<const void *>(&k_bu_spill<OffT>)
+                                 : reinterpret_cast<const void *>(&k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBS, 0) !=
                 hipSuccess ||
             per_cu < 1)
             per_cu = 4;
@@ -1970,10 +2047,14 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
                            ws->hub_id, ws->hub_k, front, ws->hfront);
         BFSX_HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>), grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col,
-                       ws->top1, ws->rest, front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords,
-                       ws->top1_flag, ws->hfront, ws->hub_id, ws->hub_lim,
-                       (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws), pub, seq);
+#define BFSX_K_BU_LAUNCH(kern)                                                                                   \
+    hipLaunchKernelGGL(kern, grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, \
+                       ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id,  \
+                       ws->hub_lim, (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws),  \
+                       pub, seq)
+    if constexpr (kSpill) BFSX_K_BU_LAUNCH((k_bu_spill<OffT>));
+    else BFSX_K_BU_LAUNCH((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>));
+#undef BFSX_K_BU_LAUNCH
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -1982,6 +2063,8 @@ template <class OffT, bool kMf, bool kHubs>
 int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
                 u64 seq) {
     if (g->ctx->opt.bu_unroll == 2) return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, level, pub, seq);
+    if (kMf && !kHubs && g->ctx->opt.bu_force_spill) // diagnostic (see k_bu's kSpill)
+        return launch_bu_u<OffT, kMf, false, 4, false, true, true>(g, ws, row_off, front, level, pub, seq);
     // kMf (partitioned) + kPipe needs more than the 96 VGPRs of 5 waves per SIMD: that instantiation runs
     // at 4 waves per SIMD (a spilling pull kernel is never an option)
     return g->ctx->opt.bu_pipeline
@@ -2084,21 +2167,10 @@ int persist_blocks(const bfsx_ctx *ctx) {
 // A frontier vertex's row is swept by ONE workgroup of K3p (kBS * kItems entries per dependent step), so a
 // frontier holding a vertex of degree > persist_dmax goes to the per-level kernels, whose multi-workgroup
 // hub bin spreads that row over the whole grid (a 5,000-entry row took 52 us in K3p, ~20 us per level).
-bool persist_fits(const bfsx_ctx *ctx, const BfsWorkspace *ws, int64_t nf, int64_t dmax) {
-    if (!ctx->opt.persist || ws->persist_off || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
-    if (dmax > ctx->opt.persist_dmax) return false;
-    const int64_t G = ws->persist_seg ? ws->persist_grid : persist_blocks(ctx);
-    if (G < 1) return false;
-    return ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
-}
-
-constexpr int kPersistAborted = -1000; // internal: K3p aborted (barrier timeout); bfs_run retries without it
-
-// Run K3p from `level` (frontier of nf vertices in ws->qa; its last frontier lands in ws->qb).
-// Returns the number of levels it ran (>= 1) with their records in the PersistOut, or an error.
-int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu) {
-    hipStream_t st = g->ctx->stream;
-    const Options &opt = g->ctx->opt;
+// K3p's buffers and grid, once per workspace: the grid is the occupancy-capped one the launch will use,
+// known before the first persist_fits test (round 2 checked the first launch's segment bound against the
+// uncapped option value).  persist_off: K3p cannot be co-resident on this device.
+int persist_setup(bfsx_graph *g, BfsWorkspace *ws) {
     if (!ws->persist_seg) {
         const int G = persist_blocks(g->ctx);
         ws->persist_grid = G;
@@ -2133,9 +2205,33 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         ws->persist_grid = std::min(G, per_cu * g->ctx->num_cus);
         if (ws->persist_grid < 1) {
             ws->persist_off = true; // cannot be co-resident: narrow levels stay per-level launches
-            return 0;
+            return BFSX_OK;
         }
     }
+    return BFSX_OK;
+}
+
+bool persist_fits(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t dmax) {
+    const bfsx_ctx *ctx = g->ctx;
+    if (!ctx->opt.persist || ws->persist_off || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
+    if (dmax > ctx->opt.persist_dmax) return false;
+    if (!ws->persist_seg && persist_setup(g, ws) != BFSX_OK) {
+        ws->persist_off = true; // no K3p buffers: narrow levels stay per-level launches
+        return false;
+    }
+    const int64_t G = ws->persist_grid;
+    if (ws->persist_off || G < 1) return false;
+    return ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
+}
+
+constexpr int kPersistAborted = -1000; // internal: K3p aborted (barrier timeout); bfs_run retries without it
+
+// Run K3p from `level` (frontier of nf vertices in ws->qa; its last frontier lands in ws->qb).
+// Returns the number of levels it ran (>= 1) with their records in the PersistOut, or an error.
+int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu) {
+    hipStream_t st = g->ctx->stream;
+    const Options &opt = g->ctx->opt;
+    if (!ws->persist_seg || ws->persist_off) return 0; // persist_fits sets K3p up before the first launch
     if (ws->persist_reset) {
         BFSX_HIP_TRY(hipMemsetAsync(ws->persist_ctl, 0, sizeof(PersistCtl), st));
         ws->persist_bar = 0;
@@ -2152,12 +2248,14 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax);
+                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
+                           (uint32_t)g->nv, ws->d_err);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax);
+                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
+                           (uint32_t)g->nv, ws->d_err);
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -2185,8 +2283,11 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
-                    (void *)ws->d_dist_ctr})
+                    (void *)ws->d_dist_ctr, (void *)ws->out_dist, (void *)ws->out_par})
         if (p) (void)hipFree(p);
+    if (ws->h_err) (void)hipHostFree(ws->h_err);
+    if (ws->ev_unpack0) (void)hipEventDestroy(ws->ev_unpack0);
+    if (ws->ev_unpack1) (void)hipEventDestroy(ws->ev_unpack1);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->h_pub) (void)hipHostFree(ws->h_pub);
     if (ws->h_pout) (void)hipHostFree(ws->h_pout);
@@ -2237,6 +2338,9 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t src_off[2];
     BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
 
+    if (opt.poison_queues) // test hook: a consumer that reads past a queue's tail meets 0xFFFFFFFF (id_ok)
+        for (uint32_t *q : {ws->qa, ws->qb, ws->hubs})
+            BFSX_HIP_TRY(hipMemsetAsync(q, 0xFF, (size_t)std::max<int64_t>(nv, 1) * sizeof(uint32_t), st));
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
@@ -2296,14 +2400,14 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         if (hybrid) {
             BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
             hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->qa,
-                               (uint32_t)nf, ws->front);
+                               (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
             BFSX_HIP_TRY(hipGetLastError());
             if (int e = launch_bu_hubonly(g, ws, ws->front, level)) return e; // -> next, vis, st
-            const Part pt{};
+            const Part pt = single_part(g, ws);
             if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true)) return e; // -> qb
             LevelSlot *cn = ws->ring + (level + 1) % 3;
             hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, cn, ws->next, ws->d_pub,
-                               ++ws->pub_seq);
+                               ++ws->pub_seq, (uint32_t)g->nv, ws->d_err);
             BFSX_HIP_TRY(hipGetLastError());
             BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
             if (int e = wait_published(ws, st)) return e;
@@ -2346,7 +2450,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             } else {
                 BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
                 hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                                   ws->qa, (uint32_t)nf, ws->front);
+                                   ws->qa, (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
             }
             BFSX_HIP_TRY(hipGetLastError());
             in_queue = false;
@@ -2376,7 +2480,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         }
         nf_core = -1;
         snapped = false;
-        if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(ctx, ws, nf, dmax)) {
+        if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
             const int ran = persist_td(g, ws, level, nf, mu);
             if (ran < 0) return ran;
@@ -2421,8 +2525,10 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                 BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
                 snapped = true;
             }
-            const Part pt{};
-            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, false, ws->d_pub, ++ws->pub_seq)) return e;
+            const Part pt = single_part(g, ws);
+            // test hook: the level's kernels read one entry past the queue's tail (the guard must catch it)
+            const int64_t nf_l = level == opt.test_overread ? nf + 1 : nf;
+            if (int e = launch_td<false>(g, ws, nf_l, mf, dmax, level, pt, false, ws->d_pub, ++ws->pub_seq)) return e;
             td_levels++;
         } else {
             if (int e = launch_bu<false>(g, ws, ws->front, level, ws->d_pub, ++ws->pub_seq)) return e;
@@ -2479,6 +2585,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
+    if (int e = check_queue_guard(ws)) return e;
     const int levels = level + 1;
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
@@ -2534,8 +2641,17 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     if (!ws || g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
     hipStream_t st = g->ctx->stream;
     const size_t nv = (size_t)g->nv;
-    // unpack into the (idle) frontier queues, then D2H
-    int32_t *d_dist = reinterpret_cast<int32_t *>(ws->qa), *d_par = reinterpret_cast<int32_t *>(ws->qb);
+    // unpack into the result's own staging buffers, then D2H.  Round 2 staged it in the frontier queues
+    // qa / qb: a consumer reading past a queue's tail then met the previous result's distances
+    // (INT32_MAX, small ints) as vertex ids ("Wrong-result events").
+    if (!ws->out_dist) {
+        BFSX_HIP_TRY(hipMalloc(&ws->out_dist, std::max<size_t>(nv, 1) * sizeof(int32_t)));
+        BFSX_HIP_TRY(hipMalloc(&ws->out_par, std::max<size_t>(nv, 1) * sizeof(int32_t)));
+        BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack0));
+        BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack1));
+    }
+    int32_t *d_dist = ws->out_dist, *d_par = ws->out_par;
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack0, st));
     if (g->d_inv)
         hipLaunchKernelGGL(k_unpack_relabel, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
                            ws->st, g->d_inv, g->v_lo, (int64_t)nv, d_dist, d_par);
@@ -2543,6 +2659,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
                            (int64_t)nv, d_dist, d_par);
     BFSX_HIP_TRY(hipGetLastError());
+    BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack1, st));
     if (dist_out) BFSX_HIP_TRY(hipMemcpyAsync(dist_out, d_dist, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (parent_out) {
         // int32 device parents land in the upper half of the int64 output, then widen in place
@@ -2554,12 +2671,19 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     } else {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
     }
+    float ms = 0.f;
+    BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_unpack0, ws->ev_unpack1));
+    ws->last_unpack_ms = ms;
     return BFSX_OK;
 }
 
+double bfs_last_unpack_ms(const bfsx_graph *g) { return g->ws ? g->ws->last_unpack_ms : -1.0; }
+
 // ==== multi-GPU level primitives (1-D partition) ====================================================
-// The level loop of a partitioned BFS runs in the caller (bfsx_dist.py over torch.distributed: RCCL
-// on device buffers), which owns the exchange buffers and passes their device pointers in:
+// The product runs the partitioned level loop natively (dist_bfs_run below, exchanges through
+// bfsx_comm.cpp).  The primitives here step the same kernels one level at a time for the test suite's
+// protocol driver (tests/dist_driver.py, include/bfsx_levels.h), which owns the exchange buffers and
+// passes their device pointers in:
 //   begin -> per level { td_expand -> all-to-all(pairs) -> td_claim | frontier_slice -> all-gather ->
 //   bu_step } -> level_end (local counts; the caller all-reduces) -> finish.
 namespace {
@@ -2571,6 +2695,8 @@ inline Part make_part(bfsx_graph *g, BfsWorkspace *ws) {
     p.rank = (uint32_t)g->rank;
     p.remote = ws->remote;
     p.remote_tail = ws->d_dist_ctr;
+    p.nrows = (uint32_t)g->nv;
+    p.err = ws->d_err;
     return p;
 }
 
@@ -2624,6 +2750,9 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
         BFSX_HIP_TRY(hipMemcpy(so, g->d_row_off + sl, sizeof(so), hipMemcpyDeviceToHost));
         deg = so[1] - so[0];
     }
+    if (g->ctx->opt.poison_queues) // test hook (see bfs_run_impl)
+        for (uint32_t *q : {ws->qa, ws->qb, ws->hubs})
+            BFSX_HIP_TRY(hipMemsetAsync(q, 0xFF, (size_t)std::max<int64_t>(g->nv, 1) * sizeof(uint32_t), st));
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
@@ -2713,10 +2842,10 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     const dim3 grid(clamp_grid((n + kBS - 1) / kBS, cap));
     if (ws->off32)
         hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, ws->off32, ws->vis,
-                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0);
+                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err);
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
-                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0);
+                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err);
     BFSX_HIP_TRY(hipGetLastError());
     return BFSX_OK;
 }
@@ -2731,7 +2860,7 @@ int dist_frontier_slice(bfsx_graph *g, u64 *d_slice) {
     if (ws->d_in_queue) {
         BFSX_HIP_TRY(hipMemsetAsync(d_slice, 0, ws->nwords * sizeof(u64), st));
         hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                           ws->qa, (uint32_t)ws->d_nf, d_slice);
+                           ws->qa, (uint32_t)ws->d_nf, d_slice, (uint32_t)g->nv, ws->d_err);
         BFSX_HIP_TRY(hipGetLastError());
     } else {
         BFSX_HIP_TRY(hipMemcpyAsync(d_slice, ws->front, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
@@ -2794,6 +2923,7 @@ int dist_finish(bfsx_graph *g) {
     BFSX_HIP_TRY(hipGetLastError());
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
+    if (int e = check_queue_guard(ws)) return e;
     {
         float ms = 0.f;
         BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
@@ -3063,11 +3193,11 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (ws->off32)
                     hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (u64)slot);
+                                       (u64)slot, (uint32_t)g->nv, ws->d_err);
                 else
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (u64)slot);
+                                       (u64)slot, (uint32_t)g->nv, ws->d_err);
                 BFSX_HIP_TRY(hipGetLastError());
             }
             td_levels++;
@@ -3079,7 +3209,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 } else {
                     BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, ws->nwords * sizeof(u64), st));
                     hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS),
-                                       0, st, ws->qa, (uint32_t)ws->d_nf, ws->front);
+                                       0, st, ws->qa, (uint32_t)ws->d_nf, ws->front, (uint32_t)g->nv, ws->d_err);
                 }
                 BFSX_HIP_TRY(hipGetLastError());
                 ws->d_in_queue = false;

@@ -177,6 +177,10 @@ int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap);
 /* Device time (ms) of the most recent BFS of g: source init -> last level complete, the stats.t_bfs_ms
  * figure without the m_comp reduction bfsx_bfs performs when stats are requested (benchmark loops). */
 int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms);
+/* Device time (ms) of the unpack kernel of the most recent bfsx_bfs / bfsx_result copy: the packed per-vertex
+ * state (internal, degree-ordered ids) -> the int32 dist and parent arrays in ORIGINAL ids that the outputs
+ * promise.  It runs after t_bfs (outside the timed region), before the D2H copy; -1 if no copy ran yet. */
+int bfsx_last_unpack_ms(const bfsx_graph *g, double *ms);
 /* Per-level direction of the most recent bfsx_bfs (BFSX_DIR_TOPDOWN / BFSX_DIR_BOTTOMUP). */
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap);
 
@@ -203,10 +207,10 @@ int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, con
  * Replaces Spark's hash-partitioned reduceByKey shuffle (BfsSpark.java:90) with an owner-routed
  * exchange.  Rank r of P holds the rows of global ids [r*chunk, r*chunk + nv_local), chunk =
  * ceil(nv/P) rounded up to 64; adjacency entries stay global.  Every rank builds its rows from the
- * same tuple list / Kronecker stream (no edge exchange at build).  The per-level exchange runs in the
- * caller (bfs-with-mapreduce_amd/bfsx_dist.py over torch.distributed = RCCL on device buffers); the
- * library provides the level primitives around it.  All buffer pointers below are DEVICE pointers
- * owned by the caller.  bfsx_bfs rejects a partitioned graph. */
+ * same tuple list / Kronecker stream (no edge exchange at build).  The whole partitioned level loop,
+ * exchanges included, runs inside the library: bfsx_dist_bfs below.  bfsx_bfs rejects a partitioned
+ * graph.  (The per-level primitives the test-suite protocol driver, tests/dist_driver.py, steps through
+ * are declared in the test-only header include/bfsx_levels.h; they are not part of this ABI.) */
 int bfsx_dist_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
                                int rank, int nranks, bfsx_graph **out);
 int bfsx_dist_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
@@ -215,27 +219,6 @@ int bfsx_graph_partition(const bfsx_graph *g, int64_t *nv_global, int64_t *v_lo,
                          int64_t *chunk, int32_t *rank, int32_t *nranks);
 /* Degree of global id v if this rank owns it (else -1). */
 int bfsx_graph_degree(const bfsx_graph *g, int64_t v, int64_t *deg);
-/* Start a BFS from global `source`; deg_local = its degree on the owning rank, 0 elsewhere. */
-int bfsx_dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local);
-/* Local frontier size and degree sum (for the caller's all-reduce and buffer sizing). */
-int bfsx_dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local);
-/* Top-down level, local part: expand the local frontier, claim owned targets, and write the
- * (v << 32 | parent) pairs for other ranks' targets into d_send, grouped by destination rank in
- * rank order; send_counts[P] receives the group sizes.  send_cap >= the local m_f is required. */
-int bfsx_dist_td_expand(bfsx_graph *g, void *d_send, int64_t send_cap, int64_t *send_counts);
-/* Claim the n pairs received from the all-to-all (all target this rank's vertices). */
-int bfsx_dist_td_claim(bfsx_graph *g, const void *d_recv, int64_t n);
-/* Write the local frontier as a bitmap slice of chunk/64 words (for the all-gather). */
-int bfsx_dist_frontier_slice(bfsx_graph *g, void *d_slice);
-/* Bottom-up level over the owned unvisited vertices against the all-gathered global frontier
- * bitmap (P * chunk/64 words). */
-int bfsx_dist_bu_step(bfsx_graph *g, const void *d_front_global);
-/* Close the level: local counts of the new frontier (the caller all-reduces them). */
-int bfsx_dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local);
-/* After the last level: unreached owned vertices -> INT32_MAX.  Results: bfsx_result (local rows). */
-int bfsx_dist_finish(bfsx_graph *g);
-/* Local share of m_comp and of the reached count (the caller all-reduces them). */
-int bfsx_dist_mcomp(bfsx_graph *g, int64_t *m_local, int64_t *reached_local);
 
 /* ---- multi-GPU, native exchange: the whole partitioned level loop inside the library ------------
  * One rank per GPU.  The exchange runs over RCCL (xGMI) on the BFS stream: top-down levels route

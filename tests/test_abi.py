@@ -12,10 +12,11 @@ import oracle_py as O
 from conftest import ROOT, load_bfsx
 
 HEADER = os.path.join(ROOT, "include", "bfsx.h")
+LEVELS_HEADER = os.path.join(ROOT, "include", "bfsx_levels.h")  # test-only level primitives
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(header=None):
+    src = "".join(open(h).read() for h in ([header] if header else [HEADER, LEVELS_HEADER]))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(bfsx_[a-z0-9_]+)\s*\(", src)))
 
@@ -27,7 +28,9 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     for n in names:
         assert hasattr(L, n), n  # ctypes attribute lookup = dlsym
-    assert sorted(bfsx.EXPORTS) == names
+    assert sorted(bfsx.EXPORTS) == declared_functions(HEADER)
+    assert sorted(bfsx.TEST_EXPORTS) == declared_functions(LEVELS_HEADER)
+    assert not set(bfsx.EXPORTS) & set(bfsx.TEST_EXPORTS)
     assert L.bfsx_abi_version() == 1
 
 

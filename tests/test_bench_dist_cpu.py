@@ -33,3 +33,29 @@ def test_bench_dist_harness_two_ranks_gloo():
     want = len(slowest) / sum(t * 1e-3 * 1e9 / m_comp for t in slowest)
     assert abs(d["value"] - want) < 1e-9 * want
     assert d["bfs_runs"] == 8 and d["config"]["parallelism"].startswith("1d-partition dp2")
+
+
+def test_bench_gpus_flag_launches_its_own_ranks():
+    """`python bench.py --gpus 2` exactly as the driver runs it (no launcher, WORLD_SIZE unset): bench.py
+    starts the two ranks itself as one torch.distributed.run child and relays the single JSON line, which
+    reports n_gpus = 2 (round 2 silently measured one GPU here)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               BFSX_BENCH_BINDING=os.path.join(ROOT, "tests", "bench_dist_fake.py"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--scale", "12", "--roots",
+                        "4", "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["bfs_runs"] == 8 and d["config"]["parallelism"].startswith("1d-partition dp2")
+
+
+def test_bench_refuses_mismatched_world_size():
+    """Inside a launcher, --gpus must equal WORLD_SIZE (exit code 2, no JSON line)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="", BFSX_BENCH_BINDING=os.path.join(ROOT, "tests", "bench_dist_fake.py"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--scale", "12"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and not r.stdout.strip(), (r.returncode, r.stdout, r.stderr[-2000:])

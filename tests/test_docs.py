@@ -1,6 +1,8 @@
 """CPU check of the documents' evidence trail: every repository path that DESIGN.md, README.md,
 INTEGRATION.md and profiles/README.md cite in backticks (profiles/, tools/, tests/, oracle/, java/,
-include/, the package) exists, so a number quoted in the design names a file the reader can open."""
+include/, the package) exists, so a number quoted in the design names a file the reader can open.  The
+same for the comments of the C-ABI headers and the native sources: every repository path or source-file
+name they cite (round 2 left `bfsx.h` naming a Python driver that had moved) exists."""
 import os
 import re
 
@@ -25,3 +27,39 @@ def test_cited_paths_exist(doc):
         if not os.path.exists(os.path.join(ROOT, path)):
             missing.append(path)
     assert not missing, f"{doc} cites missing paths: {sorted(set(missing))}"
+
+
+SOURCES = [os.path.join("include", f) for f in sorted(os.listdir(os.path.join(ROOT, "include")))] + [
+    os.path.join("bfs-with-mapreduce_amd", "csrc", f)
+    for f in sorted(os.listdir(os.path.join(ROOT, "bfs-with-mapreduce_amd", "csrc")))] + [
+    os.path.join("bfs-with-mapreduce_amd", "host", "bfsx_spark.cpp"), os.path.join("java", "bfsx_jni.c"),
+    os.path.join("bfs-with-mapreduce_amd", "bfsx.py"), "bench.py", "__graft_entry__.py"]
+
+
+def repo_basenames():
+    names = set()
+    for d, subdirs, files in os.walk(ROOT):
+        subdirs[:] = [x for x in subdirs if x not in (".git", "gpurun_out", "__pycache__", "build")]
+        names.update(files)
+    return names
+
+
+@pytest.mark.parametrize("src", SOURCES)
+def test_source_comments_cite_existing_files(src):
+    text = open(os.path.join(ROOT, src)).read()
+    lines = [ln for ln in text.splitlines() if not ln.lstrip().startswith("#include")]
+    text = "\n".join(lines)
+    names = repo_basenames()
+    missing = []
+    for m in re.finditer(r"(?<![\w/.-])(" + PREFIX + r"[\w./-]+)", text):
+        path = m.group(1).rstrip(".,;:)")
+        if "*" in path or "<" in path or path in ALLOWED or path.endswith("/") or \
+                path.startswith(("java/lang/", "java/io/")):  # JNI class names, not files
+            continue
+        if not os.path.exists(os.path.join(ROOT, path)):
+            missing.append(path)
+    # bare file names of this repository's kinds (a .py / .hip / .cpp / .sh named without a directory)
+    for m in re.finditer(r"(?<![\w/.-])([A-Za-z_][\w-]{2,}\.(?:py|hip|cpp|sh))(?![\w.])", text):
+        if m.group(1) not in names:
+            missing.append(m.group(1))
+    assert not missing, f"{src} cites missing files: {sorted(set(missing))}"
