@@ -15,12 +15,17 @@ namespace bfsx {
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
 
+#define BFSX_STR2(x) #x
+#define BFSX_STR(x) BFSX_STR2(x)
+// the message names the call and its source line: an asynchronous device fault surfaces at the next
+// checked call, and the line tells which one that was
 #define BFSX_HIP_TRY(call)                                                                   \
     do {                                                                                     \
         hipError_t e_ = (call);                                                              \
         if (e_ != hipSuccess)                                                                \
             return ::bfsx::fail(e_ == hipErrorOutOfMemory ? BFSX_E_OOM : BFSX_E_HIP,         \
-                                std::string(#call) + ": " + hipGetErrorString(e_));          \
+                                std::string(#call) + " [" + __FILE__ ":" BFSX_STR(__LINE__) "]: " + \
+                                    hipGetErrorString(e_));                                  \
     } while (0)
 
 struct Options {

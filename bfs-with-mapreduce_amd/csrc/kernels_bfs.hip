@@ -47,9 +47,10 @@ struct alignas(64) StatShard {
     u64 mu;      // bottom-up: degree sum of the candidates left unvisited (Beamer m_u, exact)
     u64 stage2;  // bottom-up: candidates that loaded rest[] (stage A2, 16 B each)
     u64 walked;  // bottom-up: adjacency entries read from col in phase B (4 B each)
+    u64 nhub;    // bottom-up, single device: vertices found below hub_row_lim (the only possible hubs)
     u64 dmax;    // top-down: largest degree in the produced frontier (skips the hub bin when <= hub_deg)
 };
-constexpr int kStatFields = 7; // summed fields, in declaration order (dmax is a max)
+constexpr int kStatFields = 8; // summed fields, in declaration order (dmax is a max)
 
 // Counters of one level.  Level L reads slot L%3 (its own frontier, already on the host), accumulates
 // the frontier it produces into slot (L+1)%3 and zeroes slot (L+2)%3: no per-level memset.
@@ -81,7 +82,7 @@ constexpr int kRecWords = 5; // per-workgroup record words of a K3p level
 // A level's counter sums as the host reads them (mapped pinned memory, written by publish_if_last).
 struct alignas(64) Published {
     u64 seq;
-    int64_t qtail, nf, mf, sc, cl, mu, dmax, stage2, walked;
+    int64_t qtail, nf, mf, sc, cl, mu, dmax, stage2, walked, nhub;
 };
 
 } // namespace
@@ -108,6 +109,11 @@ struct BfsWorkspace {
     // discovered leaf's only neighbour is its parent, so a push level after a pull level leaves the
     // leaves of its bitmap frontier out of its queue (option leaf_skip)
     int64_t leaf_lo = 0;
+    // every id >= hub_row_lim has at most hub_deg adjacency entries (the id of the last row with more, + 1;
+    // on a relabelled graph a short prefix): a pull level that found no vertex below it hands the next
+    // push level a frontier without hubs (no hub bin, K3p-eligible).  Recomputed when hub_degree changes.
+    int64_t hub_row_lim = -1;
+    uint32_t hub_row_deg = 0;
     uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
     u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
@@ -198,12 +204,12 @@ __device__ inline u64 wave_max(u64 x) {
 }
 
 __device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu, u64 dmax = 0,
-                                 u64 stage2 = 0, u64 walked = 0) {
+                                 u64 stage2 = 0, u64 walked = 0, u64 nhub = 0) {
     __shared__ u64 s_red[kStatFields][kWaves];
     __shared__ u64 s_dmax[kWaves];
     dmax = wave_max(dmax);
     if (lane_id() == 0) s_dmax[threadIdx.x >> 6] = dmax;
-    u64 v[kStatFields] = {nf, mf, scanned, claims, mu, stage2, walked};
+    u64 v[kStatFields] = {nf, mf, scanned, claims, mu, stage2, walked, nhub};
     const unsigned wave = threadIdx.x >> 6;
 #pragma unroll
     for (int f = 0; f < kStatFields; f++) {
@@ -282,13 +288,14 @@ __device__ inline void publish_if_last(LevelSlot *slot, Published *pub, u64 seq)
         auto ld = [](const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
         const u64 nf = wave_sum(ld(sh + 0)), mf = wave_sum(ld(sh + 1)), sc = wave_sum(ld(sh + 2)),
                   cl = wave_sum(ld(sh + 3)), mu = wave_sum(ld(sh + 4)), s2 = wave_sum(ld(sh + 5)),
-                  wk = wave_sum(ld(sh + 6)), dmax = wave_max(ld(sh + 7));
+                  wk = wave_sum(ld(sh + 6)), nh = wave_sum(ld(sh + 7)), dmax = wave_max(ld(sh + 8));
         const u64 qt = ld(&slot->qtail);
         if (lane == 0) {
             // mapped host memory (uncached): the record's stores complete before the sequence number's
             volatile Published *vp = pub;
             vp->stage2 = (int64_t)s2;
             vp->walked = (int64_t)wk;
+            vp->nhub = (int64_t)nh;
             vp->qtail = (int64_t)qt;
             vp->nf = (int64_t)nf;
             vp->mf = (int64_t)mf;
@@ -1168,7 +1175,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
                                             const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo,
-                                            PrefixSpec pf, Published *pub, u64 seq) {
+                                            PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ u64 s_nx[kWaves][64];
@@ -1200,7 +1207,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const int32_t nd = level + 1;
     // per-lane counters fit 32 bits (a lane sees a few hundred candidates per launch); widened at the end
-    uint32_t acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0;
+    uint32_t acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0, acc_nh = 0;
     const int64_t wstride = (int64_t)gridDim.x * kWaves * 64;
     for (int64_t w0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; w0 < nwords; w0 += wstride) {
         const int64_t wl = w0 + lane;
@@ -1332,7 +1339,10 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
                         if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
-                        else if (!kHubOnly) acc_mf += v[k] < leaf_lo ? 1u : 0u; // single device: non-leaves found
+                        else if (!kHubOnly) { // single device: non-leaves found, and possible hubs found
+                            acc_mf += v[k] < leaf_lo ? 1u : 0u;
+                            acc_nh += v[k] < hub_row_lim ? 1u : 0u;
+                        }
                     }
                     const u64 mm = __ballot(miss);
                     if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
@@ -1389,7 +1399,10 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
                             if (kMf) acc_mf += (uint32_t)(e - b);
-                            else if (!kHubOnly) acc_mf += vv < leaf_lo ? 1u : 0u;
+                            else if (!kHubOnly) {
+                                acc_mf += vv < leaf_lo ? 1u : 0u;
+                                acc_nh += vv < hub_row_lim ? 1u : 0u;
+                            }
                         } else {
                             acc_mu += (uint32_t)(e - b);
                         }
@@ -1409,7 +1422,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
         }
     }
     // claims field: rows walked (phase B)
-    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk);
+    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk, acc_nh);
     publish_if_last(cn, pub, seq);
 }
 
@@ -1418,10 +1431,10 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
         const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next,                  \
         u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level, int64_t nwords, uint32_t fmask, \
         const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo, \
-        PrefixSpec pf, Published *pub, u64 seq
+        PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim
 #define BFSX_K_BU_ARGS                                                                                          \
     row_off, col, top1, rest, front, next, vis, stt, ring, level, nwords, fmask, hfront, hub_id, hub_lim, leaf_lo, pf, \
-        pub, seq
+        pub, seq, hub_row_lim
 
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k_bu(BFSX_K_BU_PARAMS) {
@@ -1584,11 +1597,13 @@ __global__ __launch_bounds__(kBS) void k_top1(const int64_t *__restrict__ row_of
     }
 }
 
-// *out = 1 + the largest row id with two or more adjacency entries (0: none)
-__global__ __launch_bounds__(kBS) void k_leaf_lo(const int64_t *__restrict__ row_off, int64_t nv, u64 *out) {
+// *out = 1 + the largest row id with more than `thr` adjacency entries (0: none).  thr = 1: leaf_lo;
+// thr = hub_degree: hub_row_lim, below which every row of more than hub_degree entries lies
+__global__ __launch_bounds__(kBS) void k_rows_above(const int64_t *__restrict__ row_off, int64_t nv, int64_t thr,
+                                                    u64 *out) {
     u64 m = 0;
     for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS)
-        if (row_off[v + 1] - row_off[v] >= 2) m = (u64)v + 1;
+        if (row_off[v + 1] - row_off[v] > thr) m = (u64)v + 1;
     for (int d = 32; d >= 1; d >>= 1) {
         const u64 o = __shfl_xor(m, d);
         m = o > m ? o : m;
@@ -1725,7 +1740,8 @@ __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict_
 __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
                              u64 *__restrict__ ctr, int nctr) {
     for (int i = threadIdx.x; i < nctr; i += blockDim.x) ctr[i] = 0ull;
-    __shared__ u64 s[kStatFields][kShards];
+    constexpr int kSums = 7;
+    __shared__ u64 s[kSums][kShards];
     for (int i = threadIdx.x; i < kShards; i += blockDim.x) {
         s[0][i] = slot->sh[i].nf;
         s[1][i] = slot->sh[i].mf;
@@ -1736,7 +1752,7 @@ __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, in
         s[6][i] = slot->sh[i].walked;
     }
     __syncthreads();
-    if (threadIdx.x < kStatFields) {
+    if (threadIdx.x < kSums) {
         u64 t = 0;
         for (int i = 0; i < kShards; i++) t += s[threadIdx.x][i];
         if (threadIdx.x == 0 && topdown) t = slot->qtail;
@@ -1932,7 +1948,7 @@ int ws_alloc(bfsx_graph *g) {
     hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
                        ws->nwords, ws->d_red);
     BFSX_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_leaf_lo, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, ws->d_red + 1);
+    hipLaunchKernelGGL(k_rows_above, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, (int64_t)1, ws->d_red + 1);
     BFSX_HIP_TRY(hipGetLastError());
     u64 nd[2] = {0, 0};
     BFSX_HIP_TRY(hipMemcpyAsync(nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
@@ -1958,6 +1974,23 @@ int check_queue_guard(BfsWorkspace *ws) {
     *reinterpret_cast<volatile u64 *>(ws->h_err) = 0;
     return fail(BFSX_E_HIP, "internal error: a frontier-queue consumer read vertex id " +
                                 std::to_string((uint32_t)e) + ", outside the rows of this graph (stale queue entry)");
+}
+
+// ws->hub_row_lim for the current hub_degree option (one pass over the row offsets, outside any timed region).
+int ensure_hub_row_lim(bfsx_graph *g, BfsWorkspace *ws) {
+    const uint32_t hd = g->ctx->opt.hub_degree;
+    if (ws->hub_row_lim >= 0 && ws->hub_row_deg == hd) return BFSX_OK;
+    hipStream_t st = g->ctx->stream;
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
+    hipLaunchKernelGGL(k_rows_above, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, g->d_row_off,
+                       g->nv, (int64_t)hd, ws->d_red);
+    BFSX_HIP_TRY(hipGetLastError());
+    u64 lim = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&lim, ws->d_red, sizeof(lim), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    ws->hub_row_lim = (int64_t)lim;
+    ws->hub_row_deg = hd;
+    return BFSX_OK;
 }
 
 // ---- launch helpers: one per traversal kernel, dispatching on the row-offset width -------------
@@ -2051,7 +2084,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     hipLaunchKernelGGL(kern, grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, \
                        ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id,  \
                        ws->hub_lim, (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws),  \
-                       pub, seq)
+                       pub, seq, (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll))
     if constexpr (kSpill) BFSX_K_BU_LAUNCH((k_bu_spill<OffT>));
     else BFSX_K_BU_LAUNCH((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>));
 #undef BFSX_K_BU_LAUNCH
@@ -2091,7 +2124,7 @@ int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level, Publ
 }
 
 struct SlotSums {
-    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0;
+    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0, nh = 0;
 };
 
 // Spin until the level's counters of the current sequence number have landed; poll the stream now and then so a
@@ -2138,6 +2171,7 @@ SlotSums sum_slot(const LevelSlot *s) {
         r.mu += (int64_t)s->sh[i].mu;
         r.s2 += (int64_t)s->sh[i].stage2;
         r.wk += (int64_t)s->sh[i].walked;
+        r.nh += (int64_t)s->sh[i].nhub;
     }
     return r;
 }
@@ -2329,6 +2363,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int rc = ws_alloc(g);
     if (rc) return rc;
     BfsWorkspace *ws = g->ws;
+    if ((rc = ensure_hub_row_lim(g, ws))) return rc;
     bfsx_ctx *ctx = g->ctx;
     hipStream_t st = ctx->stream;
     const Options &opt = ctx->opt;
@@ -2361,6 +2396,9 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t examined = 0, visited = 1;
     // the frontier's vertices below leaf_lo (-1: unknown); set by a pull level (its k_bu counts them)
     int64_t nf_core = -1;
+    // a pull level's discoveries below hub_row_lim (-1: unknown): 0 means no frontier vertex has more than
+    // hub_degree entries, so the next push level needs no hub bin and may run inside K3p
+    int64_t nh_found = -1;
     int td_levels = 0, bu_levels = 0;
     std::vector<LevelTiming> timing;
     g->level_dirs.clear();
@@ -2436,6 +2474,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             mfh = -1;
             dir = BFSX_DIR_BOTTOMUP; // the new frontier is a bitmap
             nf_core = -1;
+            nh_found = -1;
             in_queue = false;
             snapped = false;
             bu_levels++;
@@ -2468,6 +2507,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                                ws->d_cursor, lim);
             BFSX_HIP_TRY(hipGetLastError());
             if (skip) nf = nf_core;
+            if (nh_found == 0) dmax = (int64_t)opt.hub_degree; // a bound: every discovery is a short row
             static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
             if (trace) {
                 u64 qn = 0;
@@ -2479,6 +2519,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             in_queue = true;
         }
         nf_core = -1;
+        nh_found = -1;
         snapped = false;
         if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
@@ -2572,6 +2613,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         } else {
             mu = s.mu; // exact: degree sum of the candidates this level left unvisited
             nf_core = s.mf; // the single-GPU bottom-up step counts its discoveries below leaf_lo here
+            nh_found = ws->h_pub->nhub;
             mf = -1;   // not accumulated by the single-GPU bottom-up step
             dmax = -1;
             mfh = -1;
