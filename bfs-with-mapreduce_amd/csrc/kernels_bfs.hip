@@ -167,6 +167,19 @@ struct BfsWorkspace {
 
 namespace {
 
+// Debug aid (environment BFSX_SYNC_LAUNCH=1): synchronise the stream after every launch, so an asynchronous
+// device fault surfaces at the launch that caused it (BFSX_HIP_TRY's message names the source line), while the
+// other streams -- the other ranks of an in-process group -- keep running concurrently.
+inline bool sync_launch() {
+    static const bool on = std::getenv("BFSX_SYNC_LAUNCH") != nullptr;
+    return on;
+}
+#define BFSX_LAUNCHED(stream)                                                                                   \
+    do {                                                                                                        \
+        BFSX_HIP_TRY(hipGetLastError());                                                                        \
+        if (::bfsx::sync_launch()) BFSX_HIP_TRY(hipStreamSynchronize(stream));                                  \
+    } while (0)
+
 __device__ inline unsigned lane_id() { return threadIdx.x & 63u; }
 
 __device__ inline uint32_t wave_incl_scan(uint32_t x) {
@@ -1816,12 +1829,12 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
         BFSX_HIP_TRY(hipMalloc(&slice.p, (size_t)g->chunk * sizeof(uint32_t)));
         hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, nullptr, g->nv, g->chunk,
                            (uint32_t *)slice.p);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
         if (int e = cm->allgather((const u64 *)slice.p, g->chunk / 2, (u64 *)degs.p, st)) return e;
     } else {
         hipLaunchKernelGGL(k_slice_degrees, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, nullptr, g->nv, g->nv,
                            (uint32_t *)degs.p);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
     }
     // the encoded adjacency copy (4 B per entry) and the ranking temporaries must leave half of the free
     // device memory untouched (scale 30 on one device: the graph alone is ~150 GB), else stay off (a
@@ -1852,7 +1865,7 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     HUB_ALLOC(hipMalloc(&ids2.p, nr * sizeof(uint32_t)));
     hipLaunchKernelGGL(k_hub_keys, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)degs.p, ng, (uint32_t *)keys.p,
                        (uint32_t *)ids.p);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     size_t tb = 0;
     BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)keys.p, (uint32_t *)keys2.p, (uint32_t *)ids.p,
                                            (uint32_t *)ids2.p, nr, 0, 32, st));
@@ -1866,7 +1879,7 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
     hipLaunchKernelGGL(k_count_le, dim3(gfill), dim3(kBS), 0, st, (const uint32_t *)keys2.p, ng, kth, ws->d_red);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     u64 keff = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&keff, ws->d_red, sizeof(keff), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -1881,13 +1894,13 @@ int hub_setup(bfsx_graph *g, BfsWorkspace *ws) {
     BFSX_HIP_TRY(hipMemsetAsync(hidx.p, 0xFF, nr * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_hub_index, dim3(clamp_grid((k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->hub_id, k,
                        (uint32_t *)hidx.p);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid((g->nnz + kBS - 1) / kBS, 65536)), dim3(kBS), 0, st, g->d_col,
                        g->nnz, (const uint32_t *)hidx.p, 0u, ws->colh);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     hipLaunchKernelGGL(k_hub_encode, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
                        ws->top1, g->nv, (const uint32_t *)hidx.p, ws->top1_flag, ws->top1);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipStreamSynchronize(st)); // the temporaries are freed on return
     ws->hub_k = k;
     return BFSX_OK;
@@ -1926,30 +1939,30 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_end));
     const unsigned gfill = clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192);
     hipLaunchKernelGGL(k_fill64, dim3(gfill), dim3(kBS), 0, st, ws->st, (int64_t)nv, kUnreached);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     // every offset (incl. row_off[nv] = nnz) fits in uint32; "offset_bits=64" keeps the int64 path (tests)
     if (g->nnz < (int64_t)0xFFFFFFFFll && g->ctx->opt.offset_bits != 64) {
         BFSX_HIP_TRY(hipMalloc(&ws->off32, (nv + 1) * sizeof(uint32_t)));
         hipLaunchKernelGGL(k_off32, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv + 1, ws->off32);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
     }
     ws->top1_flag = (g->nv_global <= ((int64_t)1 << 31)) ? kDeg1 : 0u;
     hipLaunchKernelGGL(k_top1, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->d_col, g->nv, ws->top1_flag, ws->top1);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     if (int e = hub_setup(g, ws)) return e;
     BFSX_HIP_TRY(hipMalloc(&ws->rest, nv * sizeof(uint4)));
     hipLaunchKernelGGL(k_rest, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, ws->hub_k > 0 ? ws->colh : g->d_col,
                        g->nv, ws->rest);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
                        g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(u64), st));
     hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
                        ws->nwords, ws->d_red);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     hipLaunchKernelGGL(k_rows_above, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, (int64_t)1, ws->d_red + 1);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     u64 nd[2] = {0, 0};
     BFSX_HIP_TRY(hipMemcpyAsync(nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -1984,7 +1997,7 @@ int ensure_hub_row_lim(bfsx_graph *g, BfsWorkspace *ws) {
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
     hipLaunchKernelGGL(k_rows_above, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, g->d_row_off,
                        g->nv, (int64_t)hd, ws->d_red);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     u64 lim = 0;
     BFSX_HIP_TRY(hipMemcpyAsync(&lim, ws->d_red, sizeof(lim), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -2021,21 +2034,21 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
                            ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip,
                            hubs ? nullptr : pub, seq);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
                                ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs, pub, seq);
-            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_LAUNCHED(st);
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip,
                            hubs ? nullptr : pub, seq);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
                                ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs, pub, seq);
-            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_LAUNCHED(st);
         }
     }
     return BFSX_OK;
@@ -2078,7 +2091,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     if (kHubs) {
         hipLaunchKernelGGL(k_hub_gather, dim3(clamp_grid((ws->hub_k + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
                            ws->hub_id, ws->hub_k, front, ws->hfront);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
     }
 #define BFSX_K_BU_LAUNCH(kern)                                                                                   \
     hipLaunchKernelGGL(kern, grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, \
@@ -2088,7 +2101,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     if constexpr (kSpill) BFSX_K_BU_LAUNCH((k_bu_spill<OffT>));
     else BFSX_K_BU_LAUNCH((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>));
 #undef BFSX_K_BU_LAUNCH
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
 
@@ -2146,7 +2159,7 @@ int wait_published(BfsWorkspace *ws, hipStream_t st) {
 // Post `na` words at a and `nb` at b to the host (in order) and wait for them; out gets na + nb words.
 int post_wait(BfsWorkspace *ws, hipStream_t st, const u64 *a, int na, const u64 *b, int nb, u64 *out) {
     hipLaunchKernelGGL(k_post, dim3(1), dim3(64), 0, st, a, na, b, nb, ws->d_post, ++ws->post_seq);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     const volatile u64 *seq = ws->h_post;
     for (uint64_t spin = 1; *seq != ws->post_seq; spin++) {
         if ((spin & 0xFFFF) == 0) {
@@ -2290,7 +2303,7 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
                            (uint32_t)g->nv, ws->d_err);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     std::atomic_thread_fence(std::memory_order_acquire);
@@ -2380,7 +2393,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
                        (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     ws->prev_source = source;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
@@ -2439,14 +2452,14 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
             hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->qa,
                                (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
-            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_LAUNCHED(st);
             if (int e = launch_bu_hubonly(g, ws, ws->front, level)) return e; // -> next, vis, st
             const Part pt = single_part(g, ws);
             if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true)) return e; // -> qb
             LevelSlot *cn = ws->ring + (level + 1) % 3;
             hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, cn, ws->next, ws->d_pub,
                                ++ws->pub_seq, (uint32_t)g->nv, ws->d_err);
-            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_LAUNCHED(st);
             BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
             if (int e = wait_published(ws, st)) return e;
             const int64_t nf_new = ws->h_pub->nf + ws->h_pub->qtail;
@@ -2491,7 +2504,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                 hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
                                    ws->qa, (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
             }
-            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_LAUNCHED(st);
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue) {
             // leaf skip: a pull level's discoveries at ids >= leaf_lo have one neighbour, their parent, so
@@ -2505,7 +2518,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             const int64_t wpb = ((cw + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
             hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, cw, wpb, ws->qa,
                                ws->d_cursor, lim);
-            BFSX_HIP_TRY(hipGetLastError());
+            BFSX_LAUNCHED(st);
             if (skip) nf = nf_core;
             if (nh_found == 0) dmax = (int64_t)opt.hub_degree; // a bound: every discovery is a short row
             static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
@@ -2624,7 +2637,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // unvisited (non-isolated) vertices -> WHITE; inside the timed region
     hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis, nwords,
                        ws->st);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
     if (int e = check_queue_guard(ws)) return e;
@@ -2668,7 +2681,7 @@ int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached) {
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(u64), st));
     hipLaunchKernelGGL(k_mcomp, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->st,
                        g->d_tuple_cnt, g->nv, ws->d_red);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipMemcpyAsync(h, ws->d_red, sizeof(h), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     *m_comp = (int64_t)h[0];
@@ -2700,7 +2713,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     else
         hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
                            (int64_t)nv, d_dist, d_par);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack1, st));
     if (dist_out) BFSX_HIP_TRY(hipMemcpyAsync(dist_out, d_dist, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (parent_out) {
@@ -2800,7 +2813,7 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
                        owned ? (uint32_t)sl : 0xFFFFFFFFu, (uint32_t)(g->v_lo + sl), ws->prev_source, ws->dead, ws->nwords,
                        ws->st, ws->vis, ws->qa, ws->ring);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     ws->prev_source = sl;
     ws->d_level = 0;
     ws->d_dir = BFSX_DIR_TOPDOWN;
@@ -2839,7 +2852,7 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
         const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
         hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
                            ws->d_cursor, ws->nwords * 64);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
         ws->d_in_queue = true;
     }
     // remote pairs <= adjacency entries of the local frontier
@@ -2862,10 +2875,10 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
         const unsigned gbk = clamp_grid(((int64_t)n_remote + kBS - 1) / kBS, 1024);
         hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                            (uint32_t)g->chunk, P, dcount);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
         hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                            (uint32_t)g->chunk, P, dcount, dcursor, d_send);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
     }
     std::vector<u64> h(P, 0);
     BFSX_HIP_TRY(hipMemcpyAsync(h.data(), dcount, P * sizeof(u64), hipMemcpyDeviceToHost, st));
@@ -2888,7 +2901,7 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
                            ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
 
@@ -2903,7 +2916,7 @@ int dist_frontier_slice(bfsx_graph *g, u64 *d_slice) {
         BFSX_HIP_TRY(hipMemsetAsync(d_slice, 0, ws->nwords * sizeof(u64), st));
         hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
                            ws->qa, (uint32_t)ws->d_nf, d_slice, (uint32_t)g->nv, ws->d_err);
-        BFSX_HIP_TRY(hipGetLastError());
+        BFSX_LAUNCHED(st);
     } else {
         BFSX_HIP_TRY(hipMemcpyAsync(d_slice, ws->front, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
     }
@@ -2962,7 +2975,7 @@ int dist_finish(bfsx_graph *g) {
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis,
                        ws->nwords, ws->st);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
     if (int e = check_queue_guard(ws)) return e;
@@ -3079,7 +3092,7 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) 
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
     hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums,
                        ws->d_dist_ctr, kCtrHead);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3, st)) return e;
     return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 16, nullptr, 0, reinterpret_cast<u64 *>(out));
@@ -3173,7 +3186,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
                 hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
                                    ws->d_cursor, ws->nwords * 64);
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
                 ws->d_in_queue = true;
             }
             // a wide top-down level may hand over to bottom-up: snapshot the visited slice (see bfs_run)
@@ -3207,18 +3220,18 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (int e = grow(ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
                 hipLaunchKernelGGL(k_bucket_slots, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, (u64)slot, dcursor, ws->sendbuf);
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
                 hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, st, dcursor, P, (u64)slot, ws->sendbuf);
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
                 plan_slots(P, slot, plan);
                 ro = P * slot; // candidate entries the claim kernel reads
             } else {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, P, dcount);
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
                 hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, P, dcount, dcursor, ws->sendbuf);
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
                 u64 *drecv = ws->d_dist_ctr + kCtrRecv;
                 if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
                     return e;
@@ -3240,7 +3253,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
                                        (u64)slot, (uint32_t)g->nv, ws->d_err);
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
             }
             td_levels++;
         } else {
@@ -3253,7 +3266,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                     hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS),
                                        0, st, ws->qa, (uint32_t)ws->d_nf, ws->front, (uint32_t)g->nv, ws->d_err);
                 }
-                BFSX_HIP_TRY(hipGetLastError());
+                BFSX_LAUNCHED(st);
                 ws->d_in_queue = false;
             }
             if (int e = cm->allgather(ws->front, ws->nwords, ws->fglob, st)) return e;
