@@ -18,7 +18,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstring>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -163,6 +166,11 @@ struct BfsWorkspace {
     int64_t d_nf = 0, d_mf = 0;
     hipEvent_t ev_start = nullptr, ev_end = nullptr;
     std::vector<hipEvent_t> ev_begin, ev_level; // per level: before / after its kernels
+    // Device buffers replaced while the partitioned loop runs (grown exchange buffers, the degree-list
+    // temporaries): freed with the workspace, never in the middle of the loop.  The ranks of an in-process
+    // group share one device, and a hipFree issued by one rank while the others' kernels ran coincided with
+    // device memory faults in those kernels ("Wrong-result events", event (b)).
+    std::vector<void *> retired;
 };
 
 namespace {
@@ -2332,6 +2340,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr, (void *)ws->out_dist, (void *)ws->out_par})
         if (p) (void)hipFree(p);
+    for (void *p : ws->retired) (void)hipFree(p);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
     if (ws->ev_unpack0) (void)hipEventDestroy(ws->ev_unpack0);
     if (ws->ev_unpack1) (void)hipEventDestroy(ws->ev_unpack1);
@@ -2858,7 +2867,7 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
     // remote pairs <= adjacency entries of the local frontier
     const int64_t need = std::max<int64_t>(ws->d_mf, 1);
     if (need > ws->remote_cap) {
-        if (ws->remote) BFSX_HIP_TRY(hipFree(ws->remote));
+        if (ws->remote) ws->retired.push_back(ws->remote);
         ws->remote = nullptr;
         ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
         BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
@@ -3006,9 +3015,57 @@ int dist_finish(bfsx_graph *g) {
 // the grouped send/recv).  Distances are level-synchronous, so they are bit-identical to bfs_run's.
 namespace {
 
-int grow(u64 *&buf, int64_t &cap, int64_t need) {
+// BFSX_TRACE / BFSX_FAULT_REPORT: the device ranges of this rank's buffers, printed (trace) or kept in a
+// registry that the fault reporter (bfsx_api.cpp) searches for the faulting address -- no output on the
+// level loop's path, so the ranks' interleaving is not disturbed.
+struct BufRange {
+    int rank;
+    const char *name;
+    uintptr_t lo, hi;
+};
+std::mutex g_buf_mu;
+std::vector<BufRange> g_bufs;
+
+// insert or replace the (rank, name) entry
+void note_range(int rank, const char *name, const void *p, int64_t bytes) {
+    std::lock_guard<std::mutex> lk(g_buf_mu);
+    const BufRange r{rank, name, (uintptr_t)p, (uintptr_t)p + (uintptr_t)std::max<int64_t>(bytes, 0)};
+    for (BufRange &x : g_bufs)
+        if (x.rank == rank && !std::strcmp(x.name, name)) {
+            x = r;
+            return;
+        }
+    g_bufs.push_back(r);
+}
+
+void note_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level, bool print) {
+    const int64_t nv = std::max<int64_t>(g->nv, 1), nw = ws->nwords;
+    const struct {
+        const char *name;
+        const void *p;
+        int64_t bytes;
+    } b[] = {{"row_off", g->d_row_off, (nv + 1) * 8},    {"col", g->d_col, g->nnz * 4},
+             {"off32", ws->off32, (nv + 1) * 4},         {"st", ws->st, nv * 8},
+             {"vis", ws->vis, nw * 8},                   {"front", ws->front, nw * 8},
+             {"next", ws->next, nw * 8},                 {"dead", ws->dead, nw * 8},
+             {"qa", ws->qa, nv * 4},                     {"qb", ws->qb, nv * 4},
+             {"hubs", ws->hubs, nv * 4},                 {"top1", ws->top1, nv * 4},
+             {"rest", ws->rest, nv * 16},                {"ring", ws->ring, 3 * (int64_t)sizeof(LevelSlot)},
+             {"remote", ws->remote, ws->remote_cap * 8}, {"sendbuf", ws->sendbuf, ws->send_cap * 8},
+             {"recvbuf", ws->recvbuf, ws->recv_cap * 8}, {"fglob", ws->fglob, ws->fglob_words * 8},
+             {"dist_ctr", ws->d_dist_ctr, kCtrWords * 8}, {"post", ws->d_post, (1 + 2 * kMaxRanks + 16) * 8},
+             {"err", ws->d_err, 8},                      {"pub", ws->d_pub, (int64_t)sizeof(Published)}};
+    for (const auto &x : b) {
+        note_range(g->rank, x.name, x.p, x.bytes);
+        if (print)
+            fprintf(stderr, "[bfsx] rank %d level %d buffer %-8s [0x%llx, 0x%llx)\n", g->rank, level, x.name,
+                    (unsigned long long)(uintptr_t)x.p, (unsigned long long)((uintptr_t)x.p + x.bytes));
+    }
+}
+
+int grow(BfsWorkspace *ws, u64 *&buf, int64_t &cap, int64_t need) {
     if (need <= cap) return BFSX_OK;
-    if (buf) BFSX_HIP_TRY(hipFree(buf));
+    if (buf) ws->retired.push_back(buf); // freed with the workspace (see BfsWorkspace::retired)
     buf = nullptr;
     cap = std::max<int64_t>(need, cap + cap / 2);
     BFSX_HIP_TRY(hipMalloc(&buf, cap * sizeof(u64)));
@@ -3027,19 +3084,27 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
     // Collective: every rank takes part in both all-gathers whatever happens locally.  Everything that can
     // fail on one rank (allocations, the selection kernels) happens before the first one, and a failed rank
     // posts the count ~0, so that all ranks leave together with the same error.
+    // the temporaries are retired into the workspace, not freed here (see BfsWorkspace::retired)
     struct Bufs {
+        std::vector<void *> &sink;
         uint32_t *slice = nullptr;
         u64 *sel = nullptr, *cnt = nullptr, *all = nullptr;
         ~Bufs() {
             for (void *p : {(void *)slice, (void *)sel, (void *)cnt, (void *)all})
-                if (p) (void)hipFree(p);
+                if (p) sink.push_back(p);
         }
-    } b;
+    } b{ws->retired};
     BFSX_HIP_TRY(hipMalloc(&b.cnt, (1 + kMaxRanks) * sizeof(u64)));
     bool ok = hipMalloc(&b.slice, g->chunk * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&b.sel, cap * sizeof(u64)) == hipSuccess &&
               hipMalloc(&b.all, (size_t)P * cap * sizeof(u64)) == hipSuccess &&
               hipMemsetAsync(b.cnt, 0, sizeof(u64), st) == hipSuccess;
+    if (std::getenv("BFSX_FAULT_REPORT")) {
+        note_range(g->rank, "big.slice (temporary)", b.slice, g->chunk * 4);
+        note_range(g->rank, "big.sel (temporary)", b.sel, (int64_t)cap * 8);
+        note_range(g->rank, "big.cnt (temporary)", b.cnt, (1 + kMaxRanks) * 8);
+        note_range(g->rank, "big.all (temporary)", b.all, (int64_t)P * cap * 8);
+    }
     if (ok) {
         hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
                            g->d_row_off, g->d_perm, g->nv, g->chunk, b.slice);
@@ -3100,6 +3165,28 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) 
 
 } // namespace
 
+// the registered buffers containing va, else the nearest one below and above it (fault reporter)
+void describe_address(uint64_t va) {
+    std::lock_guard<std::mutex> lk(g_buf_mu);
+    const BufRange *below = nullptr, *above = nullptr;
+    for (const BufRange &r : g_bufs) {
+        if (va >= r.lo && va < r.hi)
+            fprintf(stderr, "[bfsx]   inside rank %d %s [0x%llx, 0x%llx) at +%llu\n", r.rank, r.name,
+                    (unsigned long long)r.lo, (unsigned long long)r.hi, (unsigned long long)(va - r.lo));
+        if (r.hi <= va && (!below || r.hi > below->hi)) below = &r;
+        if (r.lo > va && (!above || r.lo < above->lo)) above = &r;
+    }
+    if (below)
+        fprintf(stderr, "[bfsx]   nearest below: rank %d %s [0x%llx, 0x%llx), %llu bytes past its end\n", below->rank,
+                below->name, (unsigned long long)below->lo, (unsigned long long)below->hi,
+                (unsigned long long)(va - below->hi));
+    if (above)
+        fprintf(stderr, "[bfsx]   nearest above: rank %d %s [0x%llx, 0x%llx), %llu bytes before it\n", above->rank,
+                above->name, (unsigned long long)above->lo, (unsigned long long)above->hi,
+                (unsigned long long)(above->lo - va));
+    fprintf(stderr, "[bfsx]   (%zu buffers registered)\n", g_bufs.size());
+}
+
 int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     Comm *cm = g->ctx->comm.get();
     if (!cm) return fail(BFSX_E_ARG, "no communicator on this context (bfsx_comm_init / bfsx_comm_local_group)");
@@ -3112,7 +3199,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     const Options &opt = g->ctx->opt;
     const int P = g->nranks;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
-    if (int e = grow(ws->fglob, ws->fglob_words, ws->nwords * P)) return e;
+    if (int e = grow(ws, ws->fglob, ws->fglob_words, ws->nwords * P)) return e;
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
     int64_t h[16];
     if (ws->nnz_global < 0) { // once per graph
@@ -3198,15 +3285,18 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             // remote pairs <= adjacency entries of the local frontier
             const int64_t need = std::max<int64_t>(ws->d_mf, 1);
             if (need > ws->remote_cap) {
-                if (ws->remote) BFSX_HIP_TRY(hipFree(ws->remote));
+                if (ws->remote) ws->retired.push_back(ws->remote);
                 ws->remote = nullptr;
                 ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
                 BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
             }
-            if (int e = grow(ws->sendbuf, ws->send_cap, need)) return e;
+            if (int e = grow(ws, ws->sendbuf, ws->send_cap, need)) return e;
             // the exchange counters are zero: dist_bfs_run zeroes them before the first level, every
             // level's k_level_sums after its exchange
             const Part pt = make_part(g, ws);
+            static const bool trace_bufs = std::getenv("BFSX_TRACE") != nullptr;
+            static const bool note_bufs = std::getenv("BFSX_FAULT_REPORT") != nullptr;
+            if (trace_bufs || note_bufs) note_buffers(g, ws, level, trace_bufs);
             if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, -1, level, pt)) return e;
             u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
@@ -3216,8 +3306,8 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 // small level: no rank sends more than the global m_f pairs to any peer, so every peer gets
                 // a fixed slot [count, m_f pairs] -- one exchange, no count all-to-all, no host wait
                 slot = std::max<int64_t>(mf, 1);
-                if (int e = grow(ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
-                if (int e = grow(ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
+                if (int e = grow(ws, ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
+                if (int e = grow(ws, ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
                 hipLaunchKernelGGL(k_bucket_slots, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, (u64)slot, dcursor, ws->sendbuf);
                 BFSX_LAUNCHED(st);
@@ -3238,7 +3328,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
                 plan_counted(P, hc.data(), hc.data() + P, plan);
                 ro = plan.recv_total;
-                if (int e = grow(ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
+                if (int e = grow(ws, ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
             }
             if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
                                       plan.rcount.data(), plan.rdispl.data(), st))
