@@ -26,7 +26,7 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h inclu
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(PKG)/libbfsx.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bfsx_spark: $(HOSTSRC)/bfsx_spark.cpp include/bfsx.h $(PKG)/libbfsx.so
 	$(CXX) $(CXXFLAGS) -o $@ $(HOSTSRC)/bfsx_spark.cpp -L$(PKG) -lbfsx -Wl,-rpath,'$$ORIGIN'

@@ -9,13 +9,10 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-#include <hsa/hsa_ext_amd.h>
-
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <new>
 #include <string>
 #include <unordered_set>
@@ -224,23 +221,8 @@ int bfsx_parse_algs4(const char *path, int64_t *nv_out, int64_t *m_out, uint32_t
     return BFSX_OK;
 }
 
-// Debug aid (environment BFSX_FAULT_REPORT=1): print the faulting virtual address and reason of a GPU memory
-// fault (HSA system event), to be matched against the buffer ranges BFSX_TRACE prints.
-static hsa_status_t fault_report(const hsa_amd_event_t *ev, void *) {
-    if (ev->event_type == HSA_AMD_GPU_MEMORY_FAULT_EVENT) {
-        fprintf(stderr, "[bfsx] GPU memory fault: address 0x%llx reason 0x%x\n",
-                (unsigned long long)ev->memory_fault.virtual_address, ev->memory_fault.fault_reason_mask);
-        describe_address(ev->memory_fault.virtual_address);
-    } else
-        fprintf(stderr, "[bfsx] GPU system event type %d\n", (int)ev->event_type);
-    return HSA_STATUS_SUCCESS;
-}
-
 int bfsx_init(int device, bfsx_ctx **out) {
     if (!out) return fail(BFSX_E_ARG, "null out");
-    static std::once_flag fault_once;
-    if (std::getenv("BFSX_FAULT_REPORT"))
-        std::call_once(fault_once, [] { (void)hsa_amd_register_system_event_handler(fault_report, nullptr); });
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
     if (e != hipSuccess || count <= 0) return fail(BFSX_E_NODEV, "no HIP device available");

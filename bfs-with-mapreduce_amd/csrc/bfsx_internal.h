@@ -109,7 +109,6 @@ int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
 int64_t bfs_persist_fallbacks(const bfsx_graph *g); // BFS runs re-run without K3p after a barrier abort
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
 // device time (ms) of the most recent copy's unpack kernel (packed state -> original-id dist/parent); -1: none
-void describe_address(uint64_t va); // fault reporter: registered buffers around va
 double bfs_last_unpack_ms(const bfsx_graph *g);
 // multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);

@@ -18,8 +18,6 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <cstring>
-#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -3015,30 +3013,9 @@ int dist_finish(bfsx_graph *g) {
 // the grouped send/recv).  Distances are level-synchronous, so they are bit-identical to bfs_run's.
 namespace {
 
-// BFSX_TRACE / BFSX_FAULT_REPORT: the device ranges of this rank's buffers, printed (trace) or kept in a
-// registry that the fault reporter (bfsx_api.cpp) searches for the faulting address -- no output on the
-// level loop's path, so the ranks' interleaving is not disturbed.
-struct BufRange {
-    int rank;
-    const char *name;
-    uintptr_t lo, hi;
-};
-std::mutex g_buf_mu;
-std::vector<BufRange> g_bufs;
-
-// insert or replace the (rank, name) entry
-void note_range(int rank, const char *name, const void *p, int64_t bytes) {
-    std::lock_guard<std::mutex> lk(g_buf_mu);
-    const BufRange r{rank, name, (uintptr_t)p, (uintptr_t)p + (uintptr_t)std::max<int64_t>(bytes, 0)};
-    for (BufRange &x : g_bufs)
-        if (x.rank == rank && !std::strcmp(x.name, name)) {
-            x = r;
-            return;
-        }
-    g_bufs.push_back(r);
-}
-
-void note_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level, bool print) {
+// BFSX_TRACE: the device ranges of this rank's buffers at every push level of the partitioned loop (to match
+// against a fault address or a runtime log)
+void trace_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level) {
     const int64_t nv = std::max<int64_t>(g->nv, 1), nw = ws->nwords;
     const struct {
         const char *name;
@@ -3055,12 +3032,9 @@ void note_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level, bool p
              {"recvbuf", ws->recvbuf, ws->recv_cap * 8}, {"fglob", ws->fglob, ws->fglob_words * 8},
              {"dist_ctr", ws->d_dist_ctr, kCtrWords * 8}, {"post", ws->d_post, (1 + 2 * kMaxRanks + 16) * 8},
              {"err", ws->d_err, 8},                      {"pub", ws->d_pub, (int64_t)sizeof(Published)}};
-    for (const auto &x : b) {
-        note_range(g->rank, x.name, x.p, x.bytes);
-        if (print)
-            fprintf(stderr, "[bfsx] rank %d level %d buffer %-8s [0x%llx, 0x%llx)\n", g->rank, level, x.name,
-                    (unsigned long long)(uintptr_t)x.p, (unsigned long long)((uintptr_t)x.p + x.bytes));
-    }
+    for (const auto &x : b)
+        fprintf(stderr, "[bfsx] rank %d level %d buffer %-8s [0x%llx, 0x%llx)\n", g->rank, level, x.name,
+                (unsigned long long)(uintptr_t)x.p, (unsigned long long)((uintptr_t)x.p + x.bytes));
 }
 
 int grow(BfsWorkspace *ws, u64 *&buf, int64_t &cap, int64_t need) {
@@ -3099,12 +3073,6 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
               hipMalloc(&b.sel, cap * sizeof(u64)) == hipSuccess &&
               hipMalloc(&b.all, (size_t)P * cap * sizeof(u64)) == hipSuccess &&
               hipMemsetAsync(b.cnt, 0, sizeof(u64), st) == hipSuccess;
-    if (std::getenv("BFSX_FAULT_REPORT")) {
-        note_range(g->rank, "big.slice (temporary)", b.slice, g->chunk * 4);
-        note_range(g->rank, "big.sel (temporary)", b.sel, (int64_t)cap * 8);
-        note_range(g->rank, "big.cnt (temporary)", b.cnt, (1 + kMaxRanks) * 8);
-        note_range(g->rank, "big.all (temporary)", b.all, (int64_t)P * cap * 8);
-    }
     if (ok) {
         hipLaunchKernelGGL(k_slice_degrees, dim3(clamp_grid((g->chunk + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
                            g->d_row_off, g->d_perm, g->nv, g->chunk, b.slice);
@@ -3164,28 +3132,6 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) 
 }
 
 } // namespace
-
-// the registered buffers containing va, else the nearest one below and above it (fault reporter)
-void describe_address(uint64_t va) {
-    std::lock_guard<std::mutex> lk(g_buf_mu);
-    const BufRange *below = nullptr, *above = nullptr;
-    for (const BufRange &r : g_bufs) {
-        if (va >= r.lo && va < r.hi)
-            fprintf(stderr, "[bfsx]   inside rank %d %s [0x%llx, 0x%llx) at +%llu\n", r.rank, r.name,
-                    (unsigned long long)r.lo, (unsigned long long)r.hi, (unsigned long long)(va - r.lo));
-        if (r.hi <= va && (!below || r.hi > below->hi)) below = &r;
-        if (r.lo > va && (!above || r.lo < above->lo)) above = &r;
-    }
-    if (below)
-        fprintf(stderr, "[bfsx]   nearest below: rank %d %s [0x%llx, 0x%llx), %llu bytes past its end\n", below->rank,
-                below->name, (unsigned long long)below->lo, (unsigned long long)below->hi,
-                (unsigned long long)(va - below->hi));
-    if (above)
-        fprintf(stderr, "[bfsx]   nearest above: rank %d %s [0x%llx, 0x%llx), %llu bytes before it\n", above->rank,
-                above->name, (unsigned long long)above->lo, (unsigned long long)above->hi,
-                (unsigned long long)(above->lo - va));
-    fprintf(stderr, "[bfsx]   (%zu buffers registered)\n", g_bufs.size());
-}
 
 int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     Comm *cm = g->ctx->comm.get();
@@ -3295,8 +3241,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             // level's k_level_sums after its exchange
             const Part pt = make_part(g, ws);
             static const bool trace_bufs = std::getenv("BFSX_TRACE") != nullptr;
-            static const bool note_bufs = std::getenv("BFSX_FAULT_REPORT") != nullptr;
-            if (trace_bufs || note_bufs) note_buffers(g, ws, level, trace_bufs);
+            if (trace_bufs) trace_buffers(g, ws, level);
             if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, -1, level, pt)) return e;
             u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
