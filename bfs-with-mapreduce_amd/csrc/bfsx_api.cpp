@@ -377,6 +377,13 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "bu_pipeline must be on|off");
         return BFSX_OK;
     }
+    if (k == "bu_sparse") {
+        if (v == "off") {
+            ctx->opt.bu_sparse = 0;
+            return BFSX_OK;
+        }
+        return as_int(ctx->opt.bu_sparse);
+    }
     if (k == "bu_lds_prefix") {
         if (v == "on") ctx->opt.bu_lds_prefix = true;
         else if (v == "off") ctx->opt.bu_lds_prefix = false;

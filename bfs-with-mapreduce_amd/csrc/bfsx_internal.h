@@ -42,6 +42,7 @@ struct Options {
     int hub_bits = -1;          // bottom-up hub probe domain: -1 auto, 0 off, b = 2^b hubs
     int bu_unroll = 4;          // bottom-up candidates per lane per round (4 or 2)
     bool bu_pipeline = true;    // bottom-up: the next round's top1 loads overlap this round (kU = 4)
+    int bu_sparse = 64;          // single device: pull levels with <= n/bu_sparse unvisited candidates run k_bu_sparse (0 off)
     bool bu_lds_prefix = true;  // pull kernels: the frontier bits of the 2^16 lowest (highest-degree) ids in LDS
     int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
     // partitioned: ids of degree above big_degree (at most big_cap per rank) are listed with their degree

@@ -1466,6 +1466,218 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(5))) void k
     k_bu_body<OffT, true, false, 4, false, true, true>(BFSX_K_BU_ARGS);
 }
 
+// ---- K5s: sparse pull (the tail pull levels) -------------------------------------------------------
+// A pull level whose unvisited candidates are few (a scale-26 BFS's third and later pull levels: 10^4-10^5
+// candidates in a 2^20-word bitmap) spends k_bu's time in per-group latency chains: a wave takes 64 words
+// at a time and runs the whole top1 -> probe -> rest -> probe -> row chain for the handful of candidates
+// that group holds, group after group (~3 groups per wave at scale 26: 28 us for 46 K candidates).
+// k_bu_sparse gives each wave kSparseWords consecutive words, loads them at once, gathers ALL their
+// candidates into one LDS batch list and runs the chain once per 256 candidates.  The discoveries below
+// qlim (the next push level's queue: the non-leaves with leaf_skip) are appended to qout directly, wave-
+// aggregated, so the push level that follows needs no bitmap -> queue pass; the next-frontier and visited
+// words are written back as k_bu writes them, so a pull level may follow as well.  No LDS frontier prefix:
+// with this few probes the 8 KiB copy per workgroup would cost more than it saves.
+// Counters: nf = every vertex found, mf = the ones queued (= qtail), nhub = the ones below hub_row_lim.
+constexpr int kSparseWords = 256;      // bitmap words per wave (16,384 vertices)
+constexpr uint32_t kSparseCap = 512;   // candidate batch list per wave: <= 255 carried + one window
+
+template <class OffT>
+__global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                                   const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
+                                                   const u64 *__restrict__ front, u64 *__restrict__ next,
+                                                   u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring,
+                                                   int level, int64_t nwords, uint32_t fmask, uint32_t hub_row_lim,
+                                                   uint32_t qlim, uint32_t *__restrict__ qout, Published *pub,
+                                                   u64 seq) {
+    LevelSlot *cn = ring + (level + 1) % 3;
+    zero_slot(ring, level);
+    __shared__ uint32_t s_c[kWaves][kSparseCap];
+    __shared__ uint32_t s_miss[kWaves][256];
+    __shared__ u64 s_nx[kWaves][kSparseWords];
+    const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const int32_t nd = level + 1;
+    constexpr int kC = kSparseWords / 64;
+    uint32_t acc_nf = 0, acc_q = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0, acc_nh = 0;
+    const uint32_t *front32 = reinterpret_cast<const uint32_t *>(front);
+    auto fbit = [&](uint32_t x) -> uint32_t { return (front32[x >> 5] >> (x & 31u)) & 1u; };
+    int64_t wb = 0; // first word of the wave's current range
+    // state word + next-frontier bit of a found vertex; wave-uniform queue append of the ones below qlim
+    auto settle = [&](bool found, uint32_t v, uint32_t par) {
+        if (found) {
+            stt[v] = pack_state(par, nd);
+            atomicOr(&s_nx[wave][(int64_t)(v >> 6) - wb], 1ull << (v & 63u));
+            acc_nf += 1;
+            acc_nh += v < hub_row_lim ? 1u : 0u;
+        }
+        const bool q = found && v < qlim;
+        const u64 qm = __ballot(q);
+        if (qm) {
+            const int leader = __ffsll((long long)qm) - 1;
+            u64 base = 0;
+            if ((int)lane == leader) base = atomicAdd(&cn->qtail, (u64)__popcll(qm));
+            base = __shfl(base, leader);
+            if (q) qout[base + __popcll(qm & ((1ull << lane) - 1ull))] = v;
+            acc_q += q ? 1u : 0u;
+        }
+    };
+    // one round over the first n (<= 256) ids of the wave's batch list: A1 (top1), A2 (rest), B (row walk)
+    auto run_round = [&](uint32_t n) {
+        uint32_t v[4], x[4];
+        bool ok[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t i = (uint32_t)k * 64 + lane;
+            ok[k] = i < n;
+            v[k] = ok[k] ? s_c[wave][i] : 0u;
+            x[k] = ok[k] ? top1[v[k]] : 0u;
+        }
+        uint32_t fbm = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; k++) fbm |= (ok[k] ? fbit(x[k] & ~fmask) : 0u) << k;
+        uint4 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool a2 = ok[k] && !((fbm >> k) & 1u) && !(x[k] & fmask);
+            r[k] = a2 ? rest[v[k]] : make_uint4(0u, 0u, 0u, 0u);
+            acc_s2 += a2;
+        }
+        uint32_t pbm = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (r[k].w != 0u) pbm |= (fbit(r[k].x) | (fbit(r[k].y) << 1) | (fbit(r[k].z) << 2)) << (3 * k);
+        uint32_t nmiss = 0; // wave-uniform
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            bool found = false, miss = false;
+            uint32_t par = 0;
+            const uint32_t pb = (pbm >> (3 * k)) & 7u, deg = r[k].w;
+            if (ok[k]) {
+                if ((fbm >> k) & 1u) {
+                    found = true;
+                    par = x[k] & ~fmask;
+                    acc_sc += 1;
+                } else if (x[k] & fmask) { // top1 was the row's only entry
+                    acc_mu += 1;
+                    acc_sc += 1;
+                } else if (pb) {
+                    found = true;
+                    par = (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z;
+                    acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
+                } else if (deg <= 4u) {
+                    acc_mu += deg;
+                    acc_sc += deg;
+                } else {
+                    miss = true;
+                    acc_sc += 4;
+                }
+            }
+            settle(found, v[k], par);
+            const u64 mm = __ballot(miss);
+            if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
+            nmiss += (uint32_t)__popcll(mm);
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t m0 = 0; m0 < nmiss; m0 += 64) {
+            bool found = false;
+            uint32_t par = 0, vv = 0;
+            if (m0 + lane < nmiss) {
+                vv = s_miss[wave][m0 + lane];
+                const int64_t b = (int64_t)row_off[vv], e = (int64_t)row_off[vv + 1];
+                int64_t j = b + 4;
+                while (!found && j < e) {
+                    const int64_t left = e - j;
+                    uint32_t xs[8];
+#pragma unroll
+                    for (int t = 0; t < 8; t++) xs[t] = left > t ? col[j + t] : col[j];
+                    uint32_t hm = 0u;
+#pragma unroll
+                    for (int t = 0; t < 8; t++) hm |= fbit(xs[t]) << t;
+                    if (hm) {
+                        found = true;
+                        const int h = __ffs((int)hm) - 1;
+                        par = xs[h];
+                        j += h + 1;
+                    } else {
+                        j += left < 8 ? left : 8;
+                    }
+                }
+                acc_sc += (uint32_t)(j - b - 4);
+                acc_wk += (uint32_t)(j - b - 4);
+                acc_rows += 1;
+                if (!found) acc_mu += (uint32_t)(e - b);
+            }
+            settle(found, vv, par);
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    const int64_t wstride = (int64_t)gridDim.x * kWaves * kSparseWords;
+    for (wb = ((int64_t)blockIdx.x * kWaves + wave) * kSparseWords; wb < nwords; wb += wstride) {
+        u64 vw[kC];
+#pragma unroll
+        for (int c = 0; c < kC; c++) {
+            const int64_t wl = wb + c * 64 + lane;
+            vw[c] = wl < nwords ? vis[wl] : ~0ull;
+            s_nx[wave][c * 64 + lane] = 0ull;
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t n = 0; // wave-uniform: ids waiting in the batch list
+#pragma unroll
+        for (int c = 0; c < kC; c++) {
+            const u64 unv = ~vw[c];
+            const uint32_t cnt = (uint32_t)__popcll(unv);
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t total = __shfl(incl, 63), excl = incl - cnt;
+            const uint32_t base_id = (uint32_t)((wb + c * 64 + lane) * 64);
+            for (uint32_t w0 = 0; w0 < total;) { // windows of the chunk's candidates that fit the list
+                const uint32_t take = min(total - w0, kSparseCap - n);
+                u64 bits = unv;
+                uint32_t rk = excl;
+                while (bits) {
+                    if (rk >= w0 && rk < w0 + take)
+                        s_c[wave][n + (rk - w0)] = base_id + (uint32_t)(__ffsll((long long)bits) - 1);
+                    rk++;
+                    bits &= bits - 1ull;
+                }
+                __builtin_amdgcn_wave_barrier();
+                n += take;
+                w0 += take;
+                while (n >= 256) { // full rounds, the rest moves to the front of the list
+                    run_round(256);
+                    const uint32_t left = n - 256;
+                    uint32_t keep[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t i = (uint32_t)k * 64 + lane;
+                        keep[k] = i < left ? s_c[wave][256 + i] : 0u;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t i = (uint32_t)k * 64 + lane;
+                        if (i < left) s_c[wave][i] = keep[k];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    n = left;
+                }
+            }
+        }
+        if (n) run_round(n);
+#pragma unroll
+        for (int c = 0; c < kC; c++) {
+            const int64_t wl = wb + c * 64 + lane;
+            const u64 nx = s_nx[wave][c * 64 + lane];
+            if (wl < nwords) {
+                next[wl] = nx;
+                if (nx) vis[wl] = vw[c] | nx;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // claims field: rows walked (phase B); mf field: discoveries queued
+    shard_add(cn, acc_nf, acc_q, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk, acc_nh);
+    publish_if_last(cn, pub, seq);
+}
+
 // ---- K4: frontier representation changes -------------------------------------------------------
 __global__ __launch_bounds__(kBS) void k_queue_to_bitmap(const uint32_t *__restrict__ q, uint32_t qlen, u64 *bm,
                                                          uint32_t nrows, u64 *err) {
@@ -2142,6 +2354,25 @@ int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level, Publ
                      : launch_bu_t<int64_t, kMf, false>(g, ws, g->d_row_off, front, level, pub, seq);
 }
 
+// The sparse pull kernel (tail levels): one wave per kSparseWords words.  The discoveries below qlim land in
+// ws->qa (the next push level's queue; its length is the published qtail).
+int launch_bu_sparse(bfsx_graph *g, BfsWorkspace *ws, int level, uint32_t qlim, Published *pub, u64 seq) {
+    hipStream_t st = g->ctx->stream;
+    const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
+    const dim3 grid(clamp_grid((ws->nwords + kWaves * kSparseWords - 1) / (kWaves * kSparseWords), cap));
+    const uint32_t hrl = (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll);
+    if (ws->off32)
+        hipLaunchKernelGGL(k_bu_sparse<uint32_t>, grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->top1, ws->rest,
+                           ws->front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
+                           ws->qa, pub, seq);
+    else
+        hipLaunchKernelGGL(k_bu_sparse<int64_t>, grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->top1, ws->rest,
+                           ws->front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
+                           ws->qa, pub, seq);
+    BFSX_HIP_TRY(hipGetLastError());
+    return BFSX_OK;
+}
+
 struct SlotSums {
     int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0, nh = 0;
 };
@@ -2419,6 +2650,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // a pull level's discoveries below hub_row_lim (-1: unknown): 0 means no frontier vertex has more than
     // hub_degree entries, so the next push level needs no hub bin and may run inside K3p
     int64_t nh_found = -1;
+    // the last (sparse) pull level already wrote the next push level's queue into ws->qa (nf_core ids)
+    bool queue_ready = false;
     int td_levels = 0, bu_levels = 0;
     std::vector<LevelTiming> timing;
     g->level_dirs.clear();
@@ -2450,7 +2683,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         // hybrid level costs 0.95-1.4 ms (most of it the unvisited vertices that find no frontier hub and
         // walk their whole hub prefix), the push level ~0.028 ms per million frontier edges (0.72 ms at
         // 17.6 M, 1.74 ms at 67.4 M) -- so hybrid only once the hubs' edges exceed 1.25 U.
-        bool hybrid = false;
+        bool hybrid = false, sparse = false;
         if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && has_hubs(ws) && opt.hybrid != 0 && mfh > 0) {
             const int64_t unv = nv - visited - ws->n_dead;
             hybrid = opt.hybrid == 2 || 100 * mfh > (int64_t)opt.hybrid_pct * unv;
@@ -2495,6 +2728,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             dir = BFSX_DIR_BOTTOMUP; // the new frontier is a bitmap
             nf_core = -1;
             nh_found = -1;
+            queue_ready = false;
             in_queue = false;
             snapped = false;
             bu_levels++;
@@ -2513,6 +2747,11 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             }
             BFSX_LAUNCHED(st);
             in_queue = false;
+        } else if (dir == BFSX_DIR_TOPDOWN && !in_queue && queue_ready) {
+            // the sparse pull level queued its discoveries (the non-leaves with leaf_skip) itself
+            nf = nf_core;
+            if (nh_found == 0) dmax = (int64_t)opt.hub_degree; // a bound: every discovery is a short row
+            in_queue = true;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue) {
             // leaf skip: a pull level's discoveries at ids >= leaf_lo have one neighbour, their parent, so
             // they sweep nothing; the queue holds the nf_core others (the pull kernel counted them)
@@ -2540,6 +2779,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         }
         nf_core = -1;
         nh_found = -1;
+        queue_ready = false;
         snapped = false;
         if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
@@ -2592,7 +2832,14 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             if (int e = launch_td<false>(g, ws, nf_l, mf, dmax, level, pt, false, ws->d_pub, ++ws->pub_seq)) return e;
             td_levels++;
         } else {
-            if (int e = launch_bu<false>(g, ws, ws->front, level, ws->d_pub, ++ws->pub_seq)) return e;
+            // few unvisited candidates (the tail levels): the sparse kernel, which also queues its discoveries
+            sparse = opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - ws->n_dead) * opt.bu_sparse <= nwords * 64;
+            if (sparse) {
+                const uint32_t qlim = (uint32_t)(opt.leaf_skip ? std::min<int64_t>(ws->leaf_lo, nv) : nv);
+                if (int e = launch_bu_sparse(g, ws, level, qlim, ws->d_pub, ++ws->pub_seq)) return e;
+            } else if (int e = launch_bu<false>(g, ws, ws->front, level, ws->d_pub, ++ws->pub_seq)) {
+                return e;
+            }
             bu_levels++;
         }
         BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
@@ -2606,9 +2853,10 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         s.s2 = ws->h_pub->stage2;
         s.wk = ws->h_pub->walked;
         const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? ws->h_pub->qtail : s.nf;
-        g->level_dirs.push_back(dir);
+        const int rec_dir = sparse ? BFSX_DIR_BOTTOMUP_SPARSE : dir;
+        g->level_dirs.push_back(rec_dir);
         bfsx_level_stat ls{};
-        ls.direction = dir;
+        ls.direction = rec_dir;
         ls.level = level;
         ls.frontier_in = nf;
         ls.frontier_out = nf_new;
@@ -2634,6 +2882,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             mu = s.mu; // exact: degree sum of the candidates this level left unvisited
             nf_core = s.mf; // the single-GPU bottom-up step counts its discoveries below leaf_lo here
             nh_found = ws->h_pub->nhub;
+            queue_ready = sparse; // the sparse kernel counted (mf) and queued them
             mf = -1;   // not accumulated by the single-GPU bottom-up step
             dmax = -1;
             mfh = -1;

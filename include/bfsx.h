@@ -49,6 +49,8 @@ extern "C" {
 #define BFSX_DIR_TOPDOWN 1  /* push only: the reference mapper's direction (BfsSpark.java:73-79) */
 #define BFSX_DIR_BOTTOMUP 2 /* pull only */
 #define BFSX_DIR_HYBRID 3   /* (level records only) pull from the frontier's hubs + push from its other vertices */
+#define BFSX_DIR_BOTTOMUP_SPARSE 4 /* (level records only) a pull level with few unvisited candidates, run by the
+                                     * sparse pull kernel (which also queues the next push frontier) */
 
 typedef struct bfsx_ctx bfsx_ctx;
 typedef struct bfsx_graph bfsx_graph;
@@ -69,7 +71,7 @@ typedef struct bfsx_stats {
 
 /* Per-level record of the most recent bfsx_bfs (diagnostics and roofline accounting). */
 typedef struct bfsx_level_stat {
-    int32_t direction;     /* BFSX_DIR_TOPDOWN or BFSX_DIR_BOTTOMUP */
+    int32_t direction;     /* BFSX_DIR_TOPDOWN, _BOTTOMUP, _HYBRID or _BOTTOMUP_SPARSE */
     int32_t level;         /* 0-based: expands the vertices at distance `level` */
     int64_t frontier_in;   /* vertices in the frontier being expanded (GRAY before the pass) */
     int64_t frontier_out;  /* vertices discovered (GRAY after the pass) */
@@ -112,6 +114,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "bu_unroll" = 4|2 (bottom-up candidates per lane per round)
  *   "bu_pipeline" = on|off (bottom-up: the next round's first-neighbour loads overlap the current round;
  *                 with bu_unroll 4; default on)
+ *   "bu_sparse" = int|off (single device: a pull level with at most n/bu_sparse unvisited candidates runs in
+ *                 the sparse pull kernel, which also queues the next push frontier; default 64, 1 = every pull
+ *                 level, off = never)
  *   "bu_lds_prefix" = on|off (pull kernels read the frontier bits of the 2^16 highest-degree ids of a
  *                 relabelled single-device graph from a per-workgroup LDS copy; default on)
  *   "slot_pairs" = int (partitioned graphs: a push level whose frontier has at most this many edges in

@@ -591,7 +591,8 @@ def test_leaf_skip(ctx):
                 _, _, st = check_against_oracle(g, nv, off, col, s, u, v, mr=False)
                 assert st["levels"] == 4
                 ls = g.level_stats()
-                assert [x["direction"] for x in ls] == [1, 2, 2, 1], ls
+                # the second pull level (1,000 leaves left) runs in the sparse pull kernel (direction 4)
+                assert [x["direction"] for x in ls] == [1, 2, 4, 1], ls
                 if skip == "on":
                     assert ls[3]["frontier_in"] == 0  # the leaves stayed out of the queue
                 else:
@@ -623,3 +624,33 @@ def test_leaf_skip(ctx):
         ctx.set_option("persist", "on")
         ctx.set_option("hybrid", "auto")
         ctx.set_option("leaf_skip", "on")
+
+
+@pytest.mark.parametrize("direction", ["auto", "bottomup"])
+@pytest.mark.parametrize("sparse", ["1", "64", "off"])
+def test_sparse_pull_levels(ctx, direction, sparse):
+    """The sparse pull kernel (k_bu_sparse, direction 4 in the level records): bu_sparse=1 runs EVERY pull
+    level in it, 64 (the default) the tail levels, off none.  Distances, pass counts and parents against the
+    oracle over 10 Kronecker roots, the queues poisoned (the push level after a sparse one reads the queue
+    the sparse kernel wrote), with and without the leaf skip."""
+    ou, ov = O.kronecker(15, 16, 0x5A5E)
+    nv = 1 << 15
+    off, col = O.build_sets(nv, ou, ov)
+    seen = 0
+    try:
+        ctx.set_option("direction", direction)
+        ctx.set_option("bu_sparse", sparse)
+        ctx.set_option("poison_queues", "on")
+        for skip in ("on", "off"):
+            ctx.set_option("leaf_skip", skip)
+            with ctx.kronecker(15, 16, 0x5A5E) as g:
+                for r in g.sample_roots(10, seed=11):
+                    check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=False)
+                    seen += sum(1 for d in g.level_dirs() if d == 4)
+        if sparse == "off":
+            assert seen == 0
+        else:
+            assert seen > 0
+    finally:
+        for k, val in (("direction", "auto"), ("bu_sparse", "64"), ("poison_queues", "off"), ("leaf_skip", "on")):
+            ctx.set_option(k, val)

@@ -1,6 +1,6 @@
 """Where a BFS spends its time, from bench.py --levels-json records (one list of per-level dicts with
 `root`; a new BFS starts at level 0).  Groups levels by kind (push before the first pull level, pull k,
-hybrid, push after pull) and attributes each level the time since the previous level ended (its own
+hybrid, sparse pull, push after pull) and attributes each level the time since the previous level ended (its own
 kernels plus the hand-off before them).   usage: python tools/level_breakdown.py levels.json [...]"""
 import collections
 import json
@@ -21,6 +21,9 @@ def breakdown(path):
             prev = l["cum_ms"]
             if d == 2:
                 key = "pull%d" % min(npull, 3)
+                npull += 1
+            elif d == 4:  # the sparse pull kernel (tail levels)
+                key = "pull sparse"
                 npull += 1
             elif d == 3:
                 key = "hybrid"
