@@ -78,7 +78,7 @@ constexpr int kPersistLevels = 1024;  // levels per launch
 struct alignas(64) PersistRec {
     u64 qtail, mf, dmax, scanned, claims, t_end, mfh, pad; // mfh: degree sum of the hubs discovered
 };
-constexpr int kRecWords = 5; // per-workgroup record words of a K3p level
+constexpr int kRecWords = 7; // per-workgroup record words of a K3p level
 
 // A level's counter sums as the host reads them (mapped pinned memory, written by publish_if_last).
 struct alignas(64) Published {
@@ -133,6 +133,7 @@ struct BfsWorkspace {
     // launch result (mapped pinned host memory)
     uint32_t *persist_seg = nullptr;
     u64 *persist_brec = nullptr;
+    u64 *persist_hseg = nullptr;        // heavy-row regions: 2 parities x G x kHeavyPer x {row start, v | deg << 32}
     void *persist_ctl = nullptr, *h_pout = nullptr, *d_pout = nullptr;
     int persist_grid = 0;       // workgroups (<= one per CU, all co-resident)
     size_t persist_lds = 0;     // dynamic LDS per workgroup (keeps one workgroup per CU)
@@ -182,7 +183,7 @@ inline bool sync_launch() {
 }
 #define BFSX_LAUNCHED(stream)                                                                                   \
     do {                                                                                                        \
-        BFSX_HIP_TRY(hipGetLastError());                                                                        \
+        BFSX_LAUNCHED(st);                                                                        \
         if (::bfsx::sync_launch()) BFSX_HIP_TRY(hipStreamSynchronize(stream));                                  \
     } while (0)
 
@@ -741,25 +742,123 @@ __device__ inline bool grid_sync(PersistCtl *ctl, u64 round) {
     return s_ok != 0;
 }
 
-// alpha <= 0: no direction switch (direction forced top-down).  q0: the first level's frontier
-// (contiguous); seg: 2 parities x G segments of kRegion; brec: 2 parities x G records (kRecWords);
-// qfinal: the last frontier, contiguous.  bar0: barrier rounds completed by earlier launches.
+// Heavy rows inside K3p (round 3).  A frontier vertex with more than `heavy_deg` entries is not swept by the
+// one workgroup whose slice holds it: the workgroup that discovers it records it in its own heavy region
+// (row start, vertex, degree; at most kHeavyPer per workgroup and level -- more stay light), and at the next
+// level every workgroup loads the whole heavy table (at most kHeavyMax rows) into LDS and sweeps an equal
+// 1/G share of its edges, exactly as the per-level hub bin (k_td_hubs) spreads hub rows.  So a narrow level
+// whose few vertices hold hundreds of thousands of edges -- a BFS's first and second levels -- runs inside
+// the launch instead of costing two launches and a host round trip each.  The first level's heavy row (the
+// source) comes from the host (h0_*).
+constexpr uint32_t kHeavyPer = 32;
+constexpr uint32_t kHeavyMax = 1024;
+
+// One step of K3p's sweep: kBS * kItems edges [x0, x_end) of a segment table (scan / row start / vertex, n
+// rows).  Winners store their state; light ones (<= heavy_deg entries, or a full heavy region) go to the
+// workgroup's segment, heavy ones to its heavy region (see k_td_persist).  Block-uniform.
 template <class OffT>
-__global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+__device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const uint32_t *t_scan, const int64_t *t_beg,
+                                             const uint32_t *t_u, int n, const OffT *__restrict__ row_off,
+                                             const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
+                                             int32_t nd, HubSet hs, u64 heavy_deg, uint32_t *sout, u64 *hout,
+                                             uint32_t &s_n, uint32_t &s_hn, PersistCtl *ctl, u64 &acc_mf,
+                                             u64 &attempts, u64 &acc_dmax, u64 &acc_mfh, u64 &acc_eh, u64 &acc_dmh) {
+    const unsigned tid = threadIdx.x, lane = tid & 63u;
+    uint32_t v[kItems], pu[kItems];
+    bool valid[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        const uint32_t x = x0 + (uint32_t)k * kBS + tid;
+        valid[k] = x < x_end;
+        v[k] = 0;
+        pu[k] = 0;
+        if (valid[k]) {
+            int lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (t_scan[mid] <= x) lo = mid;
+                else hi = mid - 1;
+            }
+            v[k] = col[t_beg[lo] + (int64_t)(x - t_scan[lo])];
+            pu[k] = t_u[lo];
+        }
+    }
+    // the visited word and the target's row bounds in one round trip
+    u64 wv[kItems];
+    int64_t r0[kItems], r1[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        wv[k] = valid[k] ? vis[v[k] >> 6] : ~0ull;
+        r0[k] = valid[k] ? (int64_t)row_off[v[k]] : 0;
+        r1[k] = valid[k] ? (int64_t)row_off[v[k] + 1] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        const u64 bit = 1ull << (v[k] & 63u);
+        bool win = false;
+        if (!(wv[k] & bit)) {
+            attempts++;
+            win = !(atomicOr(vis + (v[k] >> 6), bit) & bit);
+        }
+        const u64 dg = win ? (u64)(r1[k] - r0[k]) : 0ull;
+        bool heavy = false;
+        if (win) {
+            stt[v[k]] = pack_state(pu[k], nd);
+            if (dg > heavy_deg) { // a heavy row: this workgroup's heavy region, if it has room
+                const uint32_t hp = atomicAdd(&s_hn, 1u);
+                if (hp < kHeavyPer) {
+                    st_sc1(hout + 2 * hp, (u64)r0[k]);
+                    st_sc1(hout + 2 * hp + 1, (u64)v[k] | (dg << 32));
+                    heavy = true;
+                }
+            }
+        }
+        const bool light = win && !heavy;
+        acc_mf += dg;
+        acc_mfh += is_hub(hs, v[k], dg) ? dg : 0ull;
+        acc_eh += heavy ? dg : 0ull;
+        const u64 dl = light ? dg : 0ull, dh = heavy ? dg : 0ull;
+        acc_dmax = dl > acc_dmax ? dl : acc_dmax;
+        acc_dmh = dh > acc_dmh ? dh : acc_dmh;
+        const u64 mask = __ballot(light);
+        if (mask) {
+            const int leader = __ffsll((long long)mask) - 1;
+            uint32_t pos = 0;
+            if ((int)lane == leader) pos = atomicAdd(&s_n, (uint32_t)__popcll(mask));
+            pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+            if (light) {
+                if (pos < kRegion) st_sc1(sout + pos, v[k]);
+                else st_sc1(&ctl->abort, 1ull); // cannot happen: slices are bounded on entry
+            }
+        }
+    }
+}
+
+// alpha <= 0: no direction switch (direction forced top-down).  q0: the first level's (light) frontier
+// (contiguous); seg: 2 parities x G segments of kRegion; brec: 2 parities x G records (kRecWords); hseg: 2
+// parities x G heavy regions of kHeavyPer entries {row start, vertex | degree << 32}; qfinal: the last
+// frontier, contiguous (light entries, then heavy ones).  bar0: barrier rounds completed by earlier launches.
+template <class OffT>
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_td_persist(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                     const uint32_t *__restrict__ q0, uint32_t nf0, uint32_t *seg,
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
                                                     PersistOut *out, HubSet hs, int64_t bu_floor,
-                                                    int inject_abort, u64 dmax_cap, uint32_t nrows, u64 *err) {
+                                                    int inject_abort, u64 heavy_deg, uint32_t nrows, u64 *err,
+                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
+    __shared__ uint32_t s_hoff[kBS + 1];
     __shared__ uint32_t s_scan[kBS + 1];
     __shared__ int64_t s_beg[kBS];
     __shared__ uint32_t s_u[kBS];
     __shared__ uint32_t s_wsum[kWaves];
-    __shared__ u64 s_red[5][kWaves];
-    __shared__ uint32_t s_n;
+    __shared__ u64 s_red[9][kWaves];
+    __shared__ uint32_t s_n, s_hn;
+    __shared__ uint32_t s_hv[kHeavyMax];
+    __shared__ int64_t s_hb[kHeavyMax];
+    __shared__ uint32_t s_hscan[kHeavyMax + 1];
     (void)s_dyn;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const unsigned G = gridDim.x, b = blockIdx.x;
@@ -769,17 +868,66 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
         for (int i = tid; i < 3 * kSlotWords; i += kBS) p[i] = 0ull;
         if (tid == 0) out->t0 = (u64)wall_clock64();
     }
-    uint32_t nf = nf0;
+    uint32_t nf = nf0, nh_in = h0_deg ? 1u : 0u;
+    u64 eh_in = h0_deg;
     int64_t mu = mu0;
     for (int it = 0;; it++) {
         const uint32_t *sin = seg + (size_t)((it + 1) & 1) * G * kRegion; // previous level's segments
         uint32_t *sout = seg + (size_t)(it & 1) * G * kRegion + (size_t)b * kRegion;
+        const u64 *hin = hseg + (size_t)((it + 1) & 1) * G * kHeavyPer * 2;   // previous level's heavy regions
+        u64 *hout = hseg + ((size_t)(it & 1) * G + b) * kHeavyPer * 2;          // this workgroup's
         u64 *rout = brec + (size_t)(it & 1) * G * kRecWords;
         const int32_t nd = level0 + it + 1;
-        if (tid == 0) s_n = 0;
-        u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0;
+        if (tid == 0) {
+            s_n = 0;
+            s_hn = 0;
+        }
+        u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_eh = 0, acc_dmh = 0;
+        // this level's heavy table (every workgroup holds all of it)
+        if (nh_in) {
+            uint32_t d[kHeavyMax / kBS];
+            uint32_t local = 0;
+#pragma unroll
+            for (int k = 0; k < (int)(kHeavyMax / kBS); k++) {
+                const uint32_t t = tid * (kHeavyMax / kBS) + (uint32_t)k;
+                d[k] = 0;
+                if (t < nh_in) {
+                    uint32_t v = h0_v;
+                    int64_t beg = h0_beg;
+                    d[k] = h0_deg;
+                    if (it > 0) { // region r of heavy index t: the last with s_hoff[r] <= t
+                        int lo = 0, hi = (int)G - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (s_hoff[mid] <= t) lo = mid;
+                            else hi = mid - 1;
+                        }
+                        const u64 *e = hin + ((size_t)lo * kHeavyPer + (t - s_hoff[lo])) * 2;
+                        beg = (int64_t)ld_sc1(e);
+                        const u64 w = ld_sc1(e + 1);
+                        v = (uint32_t)w;
+                        d[k] = (uint32_t)(w >> 32);
+                    }
+                    s_hv[t] = v;
+                    s_hb[t] = beg;
+                }
+                local += d[k];
+            }
+            const uint32_t inc = wave_incl_scan(local);
+            if (lane == 63) s_wsum[wave] = inc;
+            __syncthreads();
+            uint32_t run = inc - local;
+            for (int w = 0; w < (int)wave; w++) run += s_wsum[w];
+#pragma unroll
+            for (int k = 0; k < (int)(kHeavyMax / kBS); k++) {
+                s_hscan[tid * (kHeavyMax / kBS) + (uint32_t)k] = run;
+                run += d[k];
+            }
+            if (tid == kBS - 1) s_hscan[kHeavyMax] = run;
+        }
         const uint32_t vb = (uint32_t)((u64)nf * b / G), ve = (uint32_t)((u64)nf * (b + 1) / G);
         __syncthreads();
+        // light rows: this workgroup's slice of the frontier, its rows swept by this workgroup
         for (uint32_t base = vb; base < ve; base += kBS) {
             const uint32_t i = base + tid;
             const int n = (int)min((uint32_t)kBS, ve - base);
@@ -820,64 +968,18 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             s_u[tid] = u;
             if (tid == 0) scanned += total;
             __syncthreads();
-            for (uint32_t x0 = 0; x0 < total; x0 += kBS * kItems) {
-                uint32_t v[kItems], pu[kItems];
-                bool valid[kItems];
-#pragma unroll
-                for (int k = 0; k < kItems; k++) {
-                    const uint32_t x = x0 + (uint32_t)k * kBS + tid;
-                    valid[k] = x < total;
-                    v[k] = 0;
-                    pu[k] = 0;
-                    if (valid[k]) {
-                        int lo = 0, hi = n - 1;
-                        while (lo < hi) {
-                            const int mid = (lo + hi + 1) >> 1;
-                            if (s_scan[mid] <= x) lo = mid;
-                            else hi = mid - 1;
-                        }
-                        v[k] = col[s_beg[lo] + (int64_t)(x - s_scan[lo])];
-                        pu[k] = s_u[lo];
-                    }
-                }
-                // the visited word and the target's row bounds in one round trip
-                u64 wv[kItems];
-                int64_t r0[kItems], r1[kItems];
-#pragma unroll
-                for (int k = 0; k < kItems; k++) {
-                    wv[k] = valid[k] ? vis[v[k] >> 6] : ~0ull;
-                    r0[k] = valid[k] ? (int64_t)row_off[v[k]] : 0;
-                    r1[k] = valid[k] ? (int64_t)row_off[v[k] + 1] : 0;
-                }
-#pragma unroll
-                for (int k = 0; k < kItems; k++) {
-                    const u64 bit = 1ull << (v[k] & 63u);
-                    bool win = false;
-                    if (!(wv[k] & bit)) {
-                        attempts++;
-                        win = !(atomicOr(vis + (v[k] >> 6), bit) & bit);
-                    }
-                    if (win) {
-                        stt[v[k]] = pack_state(pu[k], nd);
-                        const u64 dg = (u64)(r1[k] - r0[k]);
-                        acc_mf += dg;
-                        acc_dmax = dg > acc_dmax ? dg : acc_dmax;
-                        acc_mfh += is_hub(hs, v[k], dg) ? dg : 0ull;
-                    }
-                    const u64 mask = __ballot(win);
-                    if (mask) {
-                        const int leader = __ffsll((long long)mask) - 1;
-                        uint32_t pos = 0;
-                        if ((int)lane == leader) pos = atomicAdd(&s_n, (uint32_t)__popcll(mask));
-                        pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                        if (win) {
-                            if (pos < kRegion) st_sc1(sout + pos, v[k]);
-                            else st_sc1(&ctl->abort, 1ull); // cannot happen: slices are bounded on entry
-                        }
-                    }
-                }
-            }
+            for (uint32_t x0 = 0; x0 < total; x0 += kBS * kItems)
+                persist_step(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, sout, hout, s_n,
+                             s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
             __syncthreads();
+        }
+        // heavy rows: this workgroup's 1/G share of the heavy table's edges
+        if (nh_in) {
+            const uint32_t xb = (uint32_t)(eh_in * b / G), xe = (uint32_t)(eh_in * (b + 1) / G);
+            if (tid == 0) scanned += xe - xb;
+            for (uint32_t x0 = xb; x0 < xe; x0 += kBS * kItems)
+                persist_step(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, sout, hout,
+                             s_n, s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
         }
         // test hook (option "persist_abort_at"): every workgroup takes the abort path at this level, as a
         // grid-barrier timeout would, and the host re-runs the BFS without K3p
@@ -888,32 +990,40 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             }
             return;
         }
-        // this workgroup's level record
+        // this workgroup's level record: {n | light d_max << 32, m_f, scanned, claims, m_f(hubs),
+        // heavy n | heavy d_max << 32, heavy edges}
         {
             const u64 v0 = wave_sum(acc_mf), v1 = wave_sum(scanned), v2 = wave_sum(attempts), v3 = wave_max(acc_dmax),
-                      v4 = wave_sum(acc_mfh);
+                      v4 = wave_sum(acc_mfh), v5 = wave_sum(acc_eh), v6 = wave_max(acc_dmh);
             if (lane == 0) {
                 s_red[0][wave] = v0;
                 s_red[1][wave] = v1;
                 s_red[2][wave] = v2;
                 s_red[3][wave] = v3;
                 s_red[4][wave] = v4;
+                s_red[5][wave] = v5;
+                s_red[6][wave] = v6;
             }
             __syncthreads();
             if (tid == 0) {
-                u64 a = 0, c = 0, d = 0, m = 0, h = 0;
+                u64 a = 0, c = 0, d = 0, m = 0, h = 0, e = 0, mh = 0;
                 for (int w = 0; w < kWaves; w++) {
                     a += s_red[0][w];
                     c += s_red[1][w];
                     d += s_red[2][w];
                     m = s_red[3][w] > m ? s_red[3][w] : m;
                     h += s_red[4][w];
+                    e += s_red[5][w];
+                    mh = s_red[6][w] > mh ? s_red[6][w] : mh;
                 }
+                const u64 nh = min(s_hn, kHeavyPer);
                 st_sc1(rout + kRecWords * b + 0, (u64)s_n | (m << 32));
                 st_sc1(rout + kRecWords * b + 1, a);
                 st_sc1(rout + kRecWords * b + 2, c);
                 st_sc1(rout + kRecWords * b + 3, d);
                 st_sc1(rout + kRecWords * b + 4, h);
+                st_sc1(rout + kRecWords * b + 5, nh | (mh << 32));
+                st_sc1(rout + kRecWords * b + 6, e);
             }
         }
         if (!grid_sync(ctl, bar0 + (u64)it + 1)) {
@@ -923,8 +1033,8 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             }
             return;
         }
-        // every workgroup: the G records -> segment offsets and the level's sums
-        u64 r_n = 0, r_dm = 0, r_mf = 0, r_sc = 0, r_cl = 0, r_mfh = 0;
+        // every workgroup: the G records -> segment and heavy-region offsets and the level's sums
+        u64 r_n = 0, r_dm = 0, r_mf = 0, r_sc = 0, r_cl = 0, r_mfh = 0, r_nh = 0, r_dmh = 0, r_eh = 0;
         if (tid < G) {
             const u64 w0 = ld_sc1(rout + kRecWords * tid);
             r_n = w0 & 0xFFFFFFFFull;
@@ -933,40 +1043,59 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             r_sc = ld_sc1(rout + kRecWords * tid + 2);
             r_cl = ld_sc1(rout + kRecWords * tid + 3);
             r_mfh = ld_sc1(rout + kRecWords * tid + 4);
+            const u64 w5 = ld_sc1(rout + kRecWords * tid + 5);
+            r_nh = w5 & 0xFFFFFFFFull;
+            r_dmh = w5 >> 32;
+            r_eh = ld_sc1(rout + kRecWords * tid + 6);
         }
-        const uint32_t inc = wave_incl_scan((uint32_t)r_n);
+        const uint32_t inc = wave_incl_scan((uint32_t)r_n), hinc = wave_incl_scan((uint32_t)r_nh);
         const u64 smf = wave_sum(r_mf), ssc = wave_sum(r_sc), scl = wave_sum(r_cl), sdm = wave_max(r_dm),
-                  smfh = wave_sum(r_mfh);
+                  smfh = wave_sum(r_mfh), seh = wave_sum(r_eh), sdmh = wave_max(r_dmh);
+        __shared__ uint32_t s_hw[kWaves];
         __syncthreads(); // s_red / s_wsum reuse
-        if (lane == 63) s_wsum[wave] = inc;
+        if (lane == 63) {
+            s_wsum[wave] = inc;
+            s_hw[wave] = hinc;
+        }
         if (lane == 0) {
             s_red[0][wave] = smf;
             s_red[1][wave] = ssc;
             s_red[2][wave] = scl;
             s_red[3][wave] = sdm;
             s_red[4][wave] = smfh;
+            s_red[5][wave] = seh;
+            s_red[6][wave] = sdmh;
         }
         __syncthreads();
-        uint32_t woff = 0, nf_new = 0;
-        u64 mf_new = 0, sc_new = 0, cl_new = 0, dm_new = 0, mfh_new = 0;
+        uint32_t woff = 0, nf_new = 0, hoff = 0, nh_new = 0;
+        u64 mf_new = 0, sc_new = 0, cl_new = 0, dm_new = 0, mfh_new = 0, eh_new = 0, dmh_new = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; w++) {
             woff += (w < (int)wave) ? s_wsum[w] : 0u;
             nf_new += s_wsum[w];
+            hoff += (w < (int)wave) ? s_hw[w] : 0u;
+            nh_new += s_hw[w];
             mf_new += s_red[0][w];
             sc_new += s_red[1][w];
             cl_new += s_red[2][w];
             dm_new = s_red[3][w] > dm_new ? s_red[3][w] : dm_new;
             mfh_new += s_red[4][w];
+            eh_new += s_red[5][w];
+            dmh_new = s_red[6][w] > dmh_new ? s_red[6][w] : dmh_new;
         }
-        const uint32_t my_n = (uint32_t)r_n;
+        const uint32_t my_n = (uint32_t)r_n, my_nh = (uint32_t)r_nh;
         s_off[tid] = woff + inc - my_n; // entries past G: unused
-        if (tid == 0) s_off[kBS] = nf_new;
+        s_hoff[tid] = hoff + hinc - my_nh;
+        if (tid == 0) {
+            s_off[kBS] = nf_new;
+            s_hoff[kBS] = nh_new;
+        }
+        const uint32_t nf_all = nf_new + nh_new;
         if (b == 0 && tid == 0) {
             PersistRec &r = out->rec[it];
-            r.qtail = nf_new;
+            r.qtail = nf_all;
             r.mf = mf_new;
-            r.dmax = dm_new;
+            r.dmax = dm_new > dmh_new ? dm_new : dmh_new;
             r.scanned = sc_new;
             r.claims = cl_new;
             r.mfh = mfh_new;
@@ -974,17 +1103,24 @@ __global__ __launch_bounds__(kBS) void k_td_persist(const OffT *__restrict__ row
             out->levels = (u64)(it + 1);
         }
         mu -= (int64_t)mf_new;
-        const bool stop = nf_new == 0 || nf_new > kPersistNf || dm_new > dmax_cap ||
-                          (u64)((nf_new + G - 1) / G) * dm_new > (u64)kRegion ||
+        // stop when the BFS ends, the light frontier is no longer narrow, the heavy table would overflow, a
+        // workgroup's share (light slice + heavy edges) could overflow its segment, Beamer asks for
+        // bottom-up, or the level budget is used up
+        const bool stop = nf_all == 0 || nf_new > kPersistNf || nh_new > kHeavyMax ||
+                          (u64)((nf_new + G - 1) / G) * dm_new + (eh_new + G - 1) / G > (u64)kRegion ||
                           (alpha > 0 && (int64_t)mf_new > mu / alpha && (int64_t)mf_new > bu_floor) ||
                           it + 1 >= max_levels;
         __syncthreads();
-        if (stop) { // hand the frontier back contiguous
+        if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones
             const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
             for (uint32_t i = tid; i < nb; i += kBS) qfinal[ob + i] = ld_sc1(sout + i);
+            const uint32_t hb = (b + 1 < G ? s_hoff[b + 1] : nh_new) - s_hoff[b], hbase = nf_new + s_hoff[b];
+            for (uint32_t i = tid; i < hb; i += kBS) qfinal[hbase + i] = (uint32_t)ld_sc1(hout + 2 * i + 1);
             return;
         }
         nf = nf_new;
+        nh_in = nh_new;
+        eh_in = eh_new;
     }
 }
 
@@ -2369,7 +2505,7 @@ int launch_bu_sparse(bfsx_graph *g, BfsWorkspace *ws, int level, uint32_t qlim, 
         hipLaunchKernelGGL(k_bu_sparse<int64_t>, grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->top1, ws->rest,
                            ws->front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
                            ws->qa, pub, seq);
-    BFSX_HIP_TRY(hipGetLastError());
+    BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
 
@@ -2460,6 +2596,7 @@ int persist_setup(bfsx_graph *g, BfsWorkspace *ws) {
         ws->persist_grid = G;
         BFSX_HIP_TRY(hipMalloc(&ws->persist_seg, (size_t)2 * G * kRegion * sizeof(uint32_t)));
         BFSX_HIP_TRY(hipMalloc(&ws->persist_brec, (size_t)2 * G * kRecWords * sizeof(u64)));
+        BFSX_HIP_TRY(hipMalloc(&ws->persist_hseg, (size_t)2 * G * kHeavyPer * 2 * sizeof(u64)));
         BFSX_HIP_TRY(hipMalloc(&ws->persist_ctl, sizeof(PersistCtl)));
         BFSX_HIP_TRY(hipHostMalloc(&ws->h_pout, sizeof(PersistOut), hipHostMallocMapped | hipHostMallocCoherent));
         BFSX_HIP_TRY(hipHostGetDevicePointer(&ws->d_pout, ws->h_pout, 0));
@@ -2495,24 +2632,29 @@ int persist_setup(bfsx_graph *g, BfsWorkspace *ws) {
     return BFSX_OK;
 }
 
-bool persist_fits(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t dmax) {
+// heavy_src: the frontier is the source alone (level 0, its row bounds known to the host): a row longer than
+// persist_dmax enters as K3p's heavy table (spread over the whole grid) instead of keeping K3p out.
+bool persist_fits(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t dmax, bool heavy_src = false) {
     const bfsx_ctx *ctx = g->ctx;
     if (!ctx->opt.persist || ws->persist_off || nf <= 0 || nf > (int64_t)kPersistNf || dmax < 0) return false;
-    if (dmax > ctx->opt.persist_dmax) return false;
+    const bool heavy = heavy_src && nf == 1 && dmax > ctx->opt.persist_dmax;
+    if (dmax > ctx->opt.persist_dmax && !heavy) return false;
     if (!ws->persist_seg && persist_setup(g, ws) != BFSX_OK) {
         ws->persist_off = true; // no K3p buffers: narrow levels stay per-level launches
         return false;
     }
     const int64_t G = ws->persist_grid;
     if (ws->persist_off || G < 1) return false;
-    return ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
+    return heavy ? (dmax + G - 1) / G <= (int64_t)kRegion : ((nf + G - 1) / G) * dmax <= (int64_t)kRegion;
 }
 
 constexpr int kPersistAborted = -1000; // internal: K3p aborted (barrier timeout); bfs_run retries without it
 
 // Run K3p from `level` (frontier of nf vertices in ws->qa; its last frontier lands in ws->qb).
 // Returns the number of levels it ran (>= 1) with their records in the PersistOut, or an error.
-int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu) {
+// h0_deg > 0: the first level's frontier is the single heavy row {h0_v, h0_beg, h0_deg} (nf = 0 light).
+int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu, uint32_t h0_v = 0,
+               uint32_t h0_deg = 0, int64_t h0_beg = 0) {
     hipStream_t st = g->ctx->stream;
     const Options &opt = g->ctx->opt;
     if (!ws->persist_seg || ws->persist_off) return 0; // persist_fits sets K3p up before the first launch
@@ -2533,13 +2675,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -2562,7 +2704,7 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
 void bfs_workspace_free(BfsWorkspace *ws) {
     if (!ws) return;
     for (void *p : {(void *)ws->sendbuf, (void *)ws->recvbuf, (void *)ws->fglob, (void *)ws->persist_seg,
-                    (void *)ws->persist_brec, ws->persist_ctl})
+                    (void *)ws->persist_brec, (void *)ws->persist_hseg, ws->persist_ctl})
         if (p) (void)hipFree(p);
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
@@ -2781,9 +2923,12 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         nh_found = -1;
         queue_ready = false;
         snapped = false;
-        if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax)) {
+        // level 0: a source row longer than persist_dmax enters K3p as its heavy table (row bounds known)
+        const bool heavy_src = level == 0 && nf == 1 && dmax > opt.persist_dmax;
+        if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax, heavy_src)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
-            const int ran = persist_td(g, ws, level, nf, mu);
+            const int ran = heavy_src ? persist_td(g, ws, level, 0, mu, (uint32_t)source, (uint32_t)dmax, src_off[0])
+                                      : persist_td(g, ws, level, nf, mu);
             if (ran < 0) return ran;
             // ran == 0: K3p unavailable on this device (occupancy check): per-level launches below
             if (ran > 0) {

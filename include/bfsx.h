@@ -101,8 +101,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
  *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU, capped by the occupancy API so
  *                 that every workgroup is resident; fixed at a graph's first BFS)
- *   "persist_dmax" = int (the persistent launch runs only while every frontier vertex has at most this
- *                 degree; a heavier row is spread over the whole grid by the per-level kernels; default 2048)
+ *   "persist_dmax" = int (inside the persistent launch a frontier row longer than this is "heavy": the whole
+ *                 grid sweeps it, each workgroup an equal share of its edges; a frontier handed to the launch by
+ *                 the host may hold one only if it is the source alone; default 2048)
  *   "persist_abort_at" = int|off (test hook: that persistent launch aborts at its k-th level as a barrier
  *                 timeout would; the BFS is then re-run without it; default off)
  *   "hub_bits" = auto|off|1..30 (bottom-up probes of the 2^b highest-degree vertices go to a small
