@@ -183,7 +183,7 @@ inline bool sync_launch() {
 }
 #define BFSX_LAUNCHED(stream)                                                                                   \
     do {                                                                                                        \
-        BFSX_LAUNCHED(st);                                                                        \
+        BFSX_HIP_TRY(hipGetLastError());                                                                        \
         if (::bfsx::sync_launch()) BFSX_HIP_TRY(hipStreamSynchronize(stream));                                  \
     } while (0)
 
