@@ -654,3 +654,50 @@ def test_sparse_pull_levels(ctx, direction, sparse):
     finally:
         for k, val in (("direction", "auto"), ("bu_sparse", "64"), ("poison_queues", "off"), ("leaf_skip", "on")):
             ctx.set_option(k, val)
+
+
+def _star_of_hubs(nhub, fan, tail):
+    """Source 0 -> nhub hubs; hub i -> its own `fan` leaves, plus a path of `tail` vertices hanging off
+    the last leaf (a few narrow levels after the heavy ones)."""
+    hubs = 1 + np.arange(nhub)
+    leaves = 1 + nhub + np.arange(nhub * fan)
+    u = [np.zeros(nhub), np.repeat(hubs, fan)]
+    v = [hubs, leaves]
+    last = int(leaves[-1])
+    p = last + 1 + np.arange(tail)
+    u.append(np.r_[[last], p[:-1]])
+    v.append(p)
+    nv = int(p[-1]) + 1
+    return nv, np.concatenate(u).astype(np.uint32), np.concatenate(v).astype(np.uint32)
+
+
+@pytest.mark.parametrize("dmax", ["2048", "64", "8"])
+def test_persistent_heavy_rows(ctx, dmax):
+    """K3p's heavy rows (round 3): a row longer than persist_dmax is swept by the whole grid at the next
+    level (equal edge shares); the source enters as one.  Bit-exact against the oracle and against the
+    per-level kernels (persist off): a source of 6,000 hubs (every workgroup's heavy region overflows at
+    dmax 8, and the heavy table exceeds its 1,024 rows), a source of 40 hubs of 3,000 leaves (heavy rows at
+    level 1, inside the launch), and Kronecker roots."""
+    cases = [_star_of_hubs(6000, 12, 30), _star_of_hubs(40, 3000, 30)]
+    ou, ov = O.kronecker(15, 16, 0x4EA7)
+    try:
+        ctx.set_option("persist_dmax", dmax)
+        ctx.set_option("direction", "topdown")  # push levels only: every narrow level is a K3p candidate
+        ctx.set_option("poison_queues", "on")
+        for nv, u, v in cases:
+            off, col = O.build_sets(nv, u, v)
+            with ctx.from_edges(nv, u, v) as g:
+                for s in (0, 1, nv - 1):
+                    d, _, st = check_against_oracle(g, nv, off, col, s, u, v, mr=False)
+                    assert st["persist_retries"] == 0
+        nv = 1 << 15
+        off, col = O.build_sets(nv, ou, ov)
+        for direction in ("topdown", "auto"):
+            ctx.set_option("direction", direction)
+            with ctx.kronecker(15, 16, 0x4EA7) as g:
+                for r in g.sample_roots(8, seed=21):
+                    _, _, st = check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=False)
+                    assert st["persist_retries"] == 0
+    finally:
+        for k, val in (("persist_dmax", "2048"), ("direction", "auto"), ("poison_queues", "off")):
+            ctx.set_option(k, val)
