@@ -2,6 +2,7 @@
 #   libbfsx.so   : C-ABI (include/bfsx.h) + HIP kernels   -> bfs-with-mapreduce_amd/libbfsx.so
 #   bfsx_spark   : C++ host twin of BfsSpark.main          -> bfs-with-mapreduce_amd/bfsx_spark
 #   liboracle.so : CPU oracle (test infrastructure only)   -> oracle/liboracle.so
+#   fetch_calib  : FETCH_SIZE / WRITE_SIZE calibration      -> tools/fetch_calib (profiling aid)
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 PKG      := bfs-with-mapreduce_amd
@@ -15,7 +16,10 @@ KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip $(CSRC)/kernels
 HOST_SRCS   := $(CSRC)/bfsx_api.cpp $(CSRC)/bfsx_comm.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 
-all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark oracle
+all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark tools/fetch_calib oracle
+
+tools/fetch_calib: tools/fetch_calib.hip
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h include/bfsx.h
 	@mkdir -p $(OBJDIR)
@@ -35,7 +39,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(OBJDIR) $(PKG)/libbfsx.so $(PKG)/bfsx_spark
+	rm -rf $(OBJDIR) $(PKG)/libbfsx.so $(PKG)/bfsx_spark tools/fetch_calib
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
