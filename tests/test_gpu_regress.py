@@ -142,3 +142,21 @@ def test_poisoned_queues_partitioned_group(bfsx, world):
     out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, 16, 77), sources,
                     options={"poison_queues": "on"})
     check(nv, ou, ov, sources, out)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_spilling_pull_kernel_partitioned_group(bfsx, world):
+    """Round-2 event (b): the partitioned pull kernel built to spill to scratch (option bu_force_spill,
+    k_bu_spill) while the ranks of an in-process group run concurrently.  With replaced buffers retired
+    instead of freed mid-loop, the spilling build returns the oracle's distances (pull-only levels, so
+    every level runs the spilling kernel)."""
+    from test_gpu_dist_native import check, run_group
+    scale = 14
+    ou, ov = O.kronecker(scale, 16, 91)
+    nv = 1 << scale
+    off, _ = O.build_sets(nv, ou, ov)
+    deg = np.diff(off)
+    sources = [int(x) for x in np.nonzero(deg > 0)[0][[0, 11, 300]]]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, 16, 91), sources, "bottomup",
+                    options={"bu_force_spill": "on", "poison_queues": "on"})
+    check(nv, ou, ov, sources, out)
