@@ -87,7 +87,8 @@ def main():
             st = graphs[r].dist_bfs(s)
             wall = time.perf_counter() - w0
             v = graphs[r].validate()
-            lv = [{k: ls[k] for k in ("level", "direction", "frontier_in", "frontier_out", "mf_in", "kernel_ms")}
+            lv = [{k: ls[k] for k in ("level", "direction", "frontier_in", "frontier_out", "mf_in", "scanned",
+                                      "claims", "walked", "kernel_ms", "cum_ms")}
                   for ls in graphs[r].level_stats(256)]
             d = graphs[r].result()[0] if a.single else None
             return st, wall, v, lv, d
@@ -97,12 +98,12 @@ def main():
                "bottomup_levels": st["bottomup_levels"], "m_comp": st["m_comp"], "reached": st["reached"],
                "wall_ms_max_over_ranks": round(max(x[1] for x in res) * 1e3, 2),
                "validation_errors": res[0][2]["errors"], "validated_entries": res[0][2]["entries"],
-               "levels_rank0": res[0][3]}
+               "levels_rank0": res[0][3], "levels_all_ranks": [x[3] for x in res]}
         # exchange volumes implied by the level records (all ranks): a bottom-up level all-gathers the
         # n/8-byte frontier bitmap to every rank; a top-down level ships <= 8 B per remote (vertex, parent) pair
         rec["allgather_bytes_per_bu_level"] = (1 << a.scale) // 8
         out["bfs"].append(rec)
-        print(json.dumps({k: rec[k] for k in rec if k != "levels_rank0"}), flush=True)
+        print(json.dumps({k: rec[k] for k in rec if not k.startswith("levels_")}), flush=True)
         assert rec["validation_errors"] == 0
         if a.single:
             dist_parts[s] = [(graphs[r].partition()["v_lo"], res[r][4]) for r in range(P)]
