@@ -54,6 +54,8 @@ def level_bytes(ls, nwords, off_bytes=4):
     cache-resident).  off_bytes: width of the row offsets the traversal kernels read (uint32 when the
     graph has < 2^32 adjacency entries)."""
     d = ls["direction"]
+    if d == 5:  # the pass that reached only deferred degree-1 vertices (leaf_defer): no kernels of its own
+        return 0
     if d in (2, 4):  # bottom-up (4: the sparse pull kernel of the tail levels, same accounting): visited word read + next word write, top1 of every live candidate, rest[]
         # (2nd..4th neighbours + degree, 16 B) of every top1 miss, the offset pair of each row walked past
         # its first four entries (`claims`), the adjacency entries walked there, the packed state word

@@ -344,6 +344,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.test_overread = (int)x;
         return BFSX_OK;
     }
+    if (k == "leaf_defer") {
+        if (v == "on") ctx->opt.leaf_defer = true;
+        else if (v == "off") ctx->opt.leaf_defer = false;
+        else return fail(BFSX_E_ARG, "leaf_defer must be on|off");
+        return BFSX_OK;
+    }
     if (k == "leaf_skip") {
         if (v == "on") ctx->opt.leaf_skip = true;
         else if (v == "off") ctx->opt.leaf_skip = false;

@@ -49,6 +49,9 @@ struct Options {
     // on every rank (read at a graph's first partitioned BFS; see dist_big_list)
     int64_t big_degree = 4096;
     bool leaf_skip = true;      // single device: a pull level's degree-1 discoveries stay out of the next push queue
+    // single device: the degree-1 tail of the id space (ids >= leaf_lo) stays out of the level loop -- pre-visited,
+    // never claimed by a push -- and is resolved from its one neighbour after the last level (k_finalize)
+    bool leaf_defer = false;
     int64_t big_cap = (int64_t)1 << 20;
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
     int hybrid_pct = 125;       // auto: hybrid when the frontier's hub edges exceed this % of the unvisited count

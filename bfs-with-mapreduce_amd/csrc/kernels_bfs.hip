@@ -110,6 +110,14 @@ struct BfsWorkspace {
     // discovered leaf's only neighbour is its parent, so a push level after a pull level leaves the
     // leaves of its bitmap frontier out of its queue (option leaf_skip)
     int64_t leaf_lo = 0;
+    // option leaf_defer (single device): the visited-bitmap start with every id >= leaf_lo set (`dead` plus the
+    // degree-1 tail), their number, this BFS's push-claim limit (0: off) and a
+    // flag (device word: a deferred vertex lies one level beyond the core's deepest, set by k_finalize)
+    u64 *dlf = nullptr;
+    int64_t n_def = 0, leaf_hi = 0;
+    uint32_t *lt_p = nullptr, *lt_v = nullptr; // the deferred vertices (lt_v) sorted by their one neighbour (lt_p)
+    uint32_t defer_lo = 0;
+    u64 *d_leafmax = nullptr;
     // every id >= hub_row_lim has at most hub_deg adjacency entries (the id of the last row with more, + 1;
     // on a relabelled graph a short prefix): a pull level that found no vertex below it hands the next
     // push level a frontier without hubs (no hub bin, K3p-eligible).  Recomputed when hub_degree changes.
@@ -417,7 +425,10 @@ struct Part {
     u64 *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
     u64 *remote_tail; // their allocation cursor
     u64 *err;         // mapped host word: set when a queue holds an id >= nrows (null: unchecked)
+    uint32_t defer_lo; // option leaf_defer: ids >= defer_lo are never claimed by a push (0: none)
+    uint32_t pad2;
 };
+__device__ inline bool deferred(uint32_t v, uint32_t defer_lo) { return defer_lo && v >= defer_lo; }
 
 // Queue-entry guard.  Every kernel that reads vertex ids out of a frontier queue, the hub list or an
 // exchange buffer checks them against the rows it holds before using them as an index: a stale or
@@ -498,7 +509,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                 send = valid[k] && (v[k] / pt.chunk) != pt.rank;
                 vl = v[k] - pt.lo;
             }
-            if (valid[k] && !send && claim(vl, vis, attempts)) {
+            if (valid[k] && !send && !deferred(vl, pt.defer_lo) && claim(vl, vis, attempts)) {
                 win = true;
                 stt[vl] = pack_state(pu[k], nd);
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
@@ -760,8 +771,8 @@ template <class OffT>
 __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const uint32_t *t_scan, const int64_t *t_beg,
                                              const uint32_t *t_u, int n, const OffT *__restrict__ row_off,
                                              const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                             int32_t nd, HubSet hs, u64 heavy_deg, uint32_t *sout, u64 *hout,
-                                             uint32_t &s_n, uint32_t &s_hn, PersistCtl *ctl, u64 &acc_mf,
+                                             int32_t nd, HubSet hs, u64 heavy_deg, uint32_t defer_lo, uint32_t *sout,
+                                             u64 *hout, uint32_t &s_n, uint32_t &s_hn, PersistCtl *ctl, u64 &acc_mf,
                                              u64 &attempts, u64 &acc_dmax, u64 &acc_mfh, u64 &acc_eh, u64 &acc_dmh) {
     const unsigned tid = threadIdx.x, lane = tid & 63u;
     uint32_t v[kItems], pu[kItems];
@@ -781,6 +792,7 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
             }
             v[k] = col[t_beg[lo] + (int64_t)(x - t_scan[lo])];
             pu[k] = t_u[lo];
+            valid[k] = !deferred(v[k], defer_lo); // option leaf_defer: resolved after the last level
         }
     }
     // the visited word and the target's row bounds in one round trip
@@ -846,7 +858,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
                                                     PersistOut *out, HubSet hs, int64_t bu_floor,
                                                     int inject_abort, u64 heavy_deg, uint32_t nrows, u64 *err,
-                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg) {
+                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg,
+                                                    uint32_t defer_lo) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_hoff[kBS + 1];
@@ -969,7 +982,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             if (tid == 0) scanned += total;
             __syncthreads();
             for (uint32_t x0 = 0; x0 < total; x0 += kBS * kItems)
-                persist_step(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, sout, hout, s_n,
+                persist_step(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout, hout, s_n,
                              s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
             __syncthreads();
         }
@@ -978,8 +991,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             const uint32_t xb = (uint32_t)(eh_in * b / G), xe = (uint32_t)(eh_in * (b + 1) / G);
             if (tid == 0) scanned += xe - xb;
             for (uint32_t x0 = xb; x0 < xe; x0 += kBS * kItems)
-                persist_step(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, sout, hout,
-                             s_n, s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
+                persist_step(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout,
+                             hout, s_n, s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
         }
         // test hook (option "persist_abort_at"): every workgroup takes the abort path at this level, as a
         // grid-barrier timeout would, and the host re-runs the BFS without K3p
@@ -1195,9 +1208,13 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pa
 
 // Small top-down levels: pairs go to fixed per-destination slots of [count, cap pairs], so the exchange
 // needs no count all-to-all (and no host round trip) before the pairs move.
+// The slot headers (each destination's pair count) are written by the LAST workgroup to arrive on
+// `arrive` (a zeroed exchange counter), after every workgroup's cursor atomics have returned -- the round-2
+// separate k_slot_headers dispatch is gone (same fence-free hand-off as publish_if_last: the cursors are
+// device-scope atomics, read back with agent-scope loads).
 __global__ __launch_bounds__(kBS) void k_bucket_slots(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
                                                       uint32_t chunk, u64 cap, u64 *__restrict__ dcursor,
-                                                      u64 *__restrict__ out) {
+                                                      u64 *__restrict__ out, int nranks, u64 *arrive) {
     const uint64_t n = *d_n;
     for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS) {
         const u64 pr = pairs[i];
@@ -1205,9 +1222,15 @@ __global__ __launch_bounds__(kBS) void k_bucket_slots(const u64 *__restrict__ pa
         const u64 r = atomicAdd(&dcursor[d], 1ull);
         out[(u64)d * (cap + 1) + 1 + r] = pr;
     }
-}
-__global__ void k_slot_headers(const u64 *__restrict__ dcursor, int nranks, u64 cap, u64 *__restrict__ out) {
-    for (int p = threadIdx.x; p < nranks; p += blockDim.x) out[(u64)p * (cap + 1)] = dcursor[p];
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
+    __syncthreads();
+    if (!s_last) return;
+    for (int p = threadIdx.x; p < nranks; p += kBS)
+        out[(u64)p * (cap + 1)] = __hip_atomic_load(&dcursor[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
@@ -1897,14 +1920,104 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const u64 *__restrict__
 // After the last level: vertices left unvisited in this BFS (and not isolated) become WHITE again
 // (INT32_MAX, no parent), so the per-BFS init never rewrites the whole state array (isolated vertices
 // keep the value written once when the workspace is created).
-__global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ stt) {
-    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
-        u64 u = ~vis[w];
-        while (u) {
-            const int b = __ffsll((long long)u) - 1;
-            stt[w * 64 + b] = kUnreached;
-            u &= u - 1ull;
+//
+// Option leaf_defer: the same launch resolves the deferred degree-1 tail [leaf_lo, nv) (pre-visited, never
+// claimed): a non-isolated v there has exactly one neighbour u = top1[v]; v is reached iff u is -- u is the
+// source, or a core vertex (u < leaf_lo) whose visited bit is set -- and then takes parent u and u's distance
+// + 1, else it is WHITE.  The two loops touch disjoint states (unreached core vertices vs deferred ones, whose
+// parents are reached core vertices).  One coalesced top1 load and state store per deferred vertex; the
+// parents' states and visited words are the dense low-id lines.  *deep = 1 when one of them lies at
+// distance deep_d (one beyond the core's deepest: the whole BFS has one more pass).
+// Blocks [0, wblocks) sweep the visited words (grid-stride); every further block resolves kBS consecutive
+// deferred ids [leaf_lo, leaf_hi), one per thread, so the deferred range is covered in one wave of loads
+// (a grid-stride loop over it ran ~80 dependent iterations per thread: 250 us at scale 26).
+constexpr int kLeafItems = 8;
+__global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ stt,
+                                                  unsigned wblocks, const uint32_t *__restrict__ lt_p,
+                                                  const uint32_t *__restrict__ lt_v, int64_t n_lt, int64_t leaf_lo,
+                                                  uint32_t src, uint32_t deep_d, u64 *deep) {
+    if (blockIdx.x < wblocks) {
+        for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)wblocks * kBS) {
+            u64 u = ~vis[w];
+            while (u) {
+                const int b = __ffsll((long long)u) - 1;
+                stt[w * 64 + b] = kUnreached;
+                u &= u - 1ull;
+            }
         }
+        return;
+    }
+    // kLeafItems table entries per thread, strided by kBS.  The table (the deferred vertices with their one
+    // neighbour, sorted by that neighbour at workspace creation) is read coalesced and the neighbours' visited
+    // words and states in ascending order, so the gathers walk lines instead of scattering (the deferred
+    // ids themselves, in id order, have their neighbours all over the state array: 150 us at scale 26); the
+    // cost moves to the deferred vertices' own 8-B state stores, which are fire-and-forget.
+    const int64_t i0 = (int64_t)(blockIdx.x - wblocks) * kBS * kLeafItems + threadIdx.x;
+    uint32_t p[kLeafItems], v[kLeafItems];
+#pragma unroll
+    for (int k = 0; k < kLeafItems; k++) {
+        const int64_t i = i0 + (int64_t)k * kBS;
+        p[k] = i < n_lt ? lt_p[i] : 0xFFFFFFFFu;
+        v[k] = i < n_lt ? lt_v[i] : 0xFFFFFFFFu;
+    }
+    u64 vw[kLeafItems], sp[kLeafItems];
+#pragma unroll
+    for (int k = 0; k < kLeafItems; k++) {
+        const bool core = (int64_t)p[k] < leaf_lo;
+        vw[k] = core ? vis[p[k] >> 6] : 0ull;
+        sp[k] = core ? stt[p[k]] : 0ull;
+    }
+    bool is_deep = false;
+#pragma unroll
+    for (int k = 0; k < kLeafItems; k++) {
+        if (v[k] == 0xFFFFFFFFu || v[k] == src) continue;
+        const bool core = (int64_t)p[k] < leaf_lo;
+        u64 s = kUnreached;
+        if (p[k] == src) {
+            s = pack_state(p[k], 1);
+            is_deep |= deep_d == 1u;
+        } else if (core && ((vw[k] >> (p[k] & 63u)) & 1ull)) {
+            const uint32_t d = (uint32_t)sp[k] + 1u;
+            s = pack_state(p[k], (int32_t)d);
+            is_deep |= d == deep_d;
+        }
+        stt[v[k]] = s;
+    }
+    // a deferred vertex one level beyond the core's deepest: the whole BFS has one more pass.  One plain store
+    // of the same value per wave that holds one (an atomic max per wave serialised 134 K same-address atomics:
+    // 1.5 ms at scale 26)
+    const u64 dm = __ballot(is_deep);
+    if (dm && (int)lane_id() == __ffsll((long long)dm) - 1) *deep = 1ull;
+}
+
+// leaf table keys: the one neighbour of every deferred vertex (~0 for a self-loop-only row: not a leaf)
+__global__ __launch_bounds__(kBS) void k_leaf_keys(const uint32_t *__restrict__ top1, uint32_t flag, int64_t lo,
+                                                   int64_t n, uint32_t *__restrict__ key, uint32_t *__restrict__ val) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        const uint32_t v = (uint32_t)(lo + i), p = top1[lo + i] & ~flag;
+        key[i] = p == v ? 0xFFFFFFFFu : p;
+        val[i] = v;
+    }
+}
+
+// 1 + the largest id whose row holds an entry other than itself (the end of the deferred range)
+__global__ __launch_bounds__(kBS) void k_last_live(const u64 *__restrict__ dead, int64_t nwords, u64 *out) {
+    u64 best = 0;
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
+        const u64 m = ~dead[w];
+        if (m) best = max(best, (u64)(w * 64 + 64 - __clzll((long long)m)));
+    }
+    best = wave_max(best);
+    if (lane_id() == 0 && best) atomicMax(out, best);
+}
+
+// leaf_defer: the BFS's starting visited bitmap = dead | every id >= leaf_lo
+__global__ __launch_bounds__(kBS) void k_leaf_mask(const u64 *__restrict__ dead, int64_t nwords, int64_t leaf_lo,
+                                                   u64 *__restrict__ out) {
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
+        const int64_t b = w * 64;
+        const u64 m = b >= leaf_lo ? ~0ull : (b + 64 <= leaf_lo ? 0ull : ~0ull << (leaf_lo - b));
+        out[w] = dead[w] | m;
     }
 }
 
@@ -2322,6 +2435,50 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     ws->n_dead = (int64_t)nd[0] - (ws->nwords * 64 - g->nv); // minus padding bits
     ws->leaf_lo = (int64_t)nd[1];
+    if (g->nranks == 1 && ws->leaf_lo < g->nv) { // option leaf_defer: the start bitmap with the degree-1 tail set
+        BFSX_HIP_TRY(hipMalloc(&ws->dlf, ws->nwords * sizeof(u64)));
+        BFSX_HIP_TRY(hipMalloc(&ws->d_leafmax, sizeof(u64)));
+        hipLaunchKernelGGL(k_leaf_mask, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
+                           ws->dead, ws->nwords, ws->leaf_lo, ws->dlf);
+        BFSX_LAUNCHED(st);
+        BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
+        hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dlf,
+                           ws->nwords, ws->d_red);
+        BFSX_LAUNCHED(st);
+        BFSX_HIP_TRY(hipMemsetAsync(ws->d_red + 1, 0, sizeof(u64), st));
+        hipLaunchKernelGGL(k_last_live, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st,
+                           ws->dead, ws->nwords, ws->d_red + 1);
+        BFSX_LAUNCHED(st);
+        u64 nl[2] = {0, 0};
+        BFSX_HIP_TRY(hipMemcpyAsync(nl, ws->d_red, sizeof(nl), hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        ws->n_def = (int64_t)nl[0] - (int64_t)nd[0]; // the deferred (non-isolated) vertices
+        ws->leaf_hi = std::max<int64_t>(std::min<int64_t>((int64_t)nl[1], g->nv), ws->leaf_lo);
+        // the leaf table: (neighbour, vertex) of every deferred vertex, sorted by neighbour (k_finalize)
+        const int64_t nr = ws->leaf_hi - ws->leaf_lo;
+        if (nr > 0) {
+            struct Tmp {
+                void *p = nullptr;
+                ~Tmp() {
+                    if (p) (void)hipFree(p);
+                }
+            } k1, v1, tmp;
+            BFSX_HIP_TRY(hipMalloc(&k1.p, nr * sizeof(uint32_t)));
+            BFSX_HIP_TRY(hipMalloc(&v1.p, nr * sizeof(uint32_t)));
+            BFSX_HIP_TRY(hipMalloc(&ws->lt_p, nr * sizeof(uint32_t)));
+            BFSX_HIP_TRY(hipMalloc(&ws->lt_v, nr * sizeof(uint32_t)));
+            hipLaunchKernelGGL(k_leaf_keys, dim3(clamp_grid((nr + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->top1,
+                               ws->top1_flag, ws->leaf_lo, nr, (uint32_t *)k1.p, (uint32_t *)v1.p);
+            BFSX_LAUNCHED(st);
+            size_t tb = 0;
+            BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)k1.p, ws->lt_p, (uint32_t *)v1.p, ws->lt_v,
+                                                   (size_t)nr, 0, 32, st));
+            BFSX_HIP_TRY(hipMalloc(&tmp.p, std::max<size_t>(tb, 16)));
+            BFSX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tb, (uint32_t *)k1.p, ws->lt_p, (uint32_t *)v1.p, ws->lt_v,
+                                                   (size_t)nr, 0, 32, st));
+            BFSX_HIP_TRY(hipStreamSynchronize(st)); // the temporaries are freed at the end of this scope
+        }
+    }
     return BFSX_OK;
 }
 
@@ -2330,6 +2487,7 @@ Part single_part(const bfsx_graph *g, const BfsWorkspace *ws) {
     Part p{};
     p.nrows = (uint32_t)g->nv;
     p.err = ws->d_err;
+    p.defer_lo = ws->defer_lo;
     return p;
 }
 
@@ -2675,13 +2833,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
     else
         hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -2709,7 +2867,8 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
-                    (void *)ws->d_dist_ctr, (void *)ws->out_dist, (void *)ws->out_par})
+                    (void *)ws->d_dist_ctr, (void *)ws->out_dist, (void *)ws->out_par, (void *)ws->dlf,
+                    (void *)ws->d_leafmax, (void *)ws->lt_p, (void *)ws->lt_v})
         if (p) (void)hipFree(p);
     for (void *p : ws->retired) (void)hipFree(p);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
@@ -2766,13 +2925,23 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t src_off[2];
     BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
 
+    // option leaf_defer: the degree-1 tail starts visited and is resolved by k_finalize
+    // (not with the encoded hub probe domain of a graph built without the relabel: its top1 holds encoded ids)
+    const bool defer = opt.leaf_defer && ws->dlf != nullptr && ws->hub_k == 0;
+    ws->defer_lo = defer ? (uint32_t)ws->leaf_lo : 0u;
+    const int64_t n_pre = ws->n_dead + (defer ? ws->n_def : 0); // pre-visited non-padding ids
+    // Beamer's n of the pull -> push rule: with the tail deferred, n_f counts core vertices only, so the rule
+    // compares it with the core vertices (the ids neither isolated nor deferred)
+    const int64_t nbeta = defer ? std::max<int64_t>(g->nv - n_pre, 1) : g->nv;
+    if (defer) BFSX_HIP_TRY(hipMemsetAsync(ws->d_leafmax, 0, sizeof(u64), st));
     if (opt.poison_queues) // test hook: a consumer that reads past a queue's tail meets 0xFFFFFFFF (id_ok)
         for (uint32_t *q : {ws->qa, ws->qb, ws->hubs})
             BFSX_HIP_TRY(hipMemsetAsync(q, 0xFF, (size_t)std::max<int64_t>(nv, 1) * sizeof(uint32_t), st));
     // ---- timed region: source init -> last level ----
     BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
-                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring);
+                       (uint32_t)source, ws->prev_source, defer ? ws->dlf : ws->dead, nwords, ws->st, ws->vis, ws->qa,
+                       ws->ring);
     BFSX_LAUNCHED(st);
     ws->prev_source = source;
 
@@ -2804,7 +2973,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         if (opt.direction == BFSX_DIR_AUTO && level > 0) {
             if (dir == BFSX_DIR_TOPDOWN) {
                 if (mf > mu / std::max(opt.alpha, 1) && mf > bu_floor(ws)) dir = BFSX_DIR_BOTTOMUP;
-            } else if (nf < nv / std::max(opt.beta, 1) && nf < prev_nf) {
+            } else if (nf < nbeta / std::max(opt.beta, 1) && nf < prev_nf) {
                 dir = BFSX_DIR_TOPDOWN;
             }
         }
@@ -2827,7 +2996,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         // 17.6 M, 1.74 ms at 67.4 M) -- so hybrid only once the hubs' edges exceed 1.25 U.
         bool hybrid = false, sparse = false;
         if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && has_hubs(ws) && opt.hybrid != 0 && mfh > 0) {
-            const int64_t unv = nv - visited - ws->n_dead;
+            const int64_t unv = nv - visited - n_pre;
             hybrid = opt.hybrid == 2 || 100 * mfh > (int64_t)opt.hybrid_pct * unv;
         }
         if (hybrid) {
@@ -2852,7 +3021,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             ls.frontier_in = nf;
             ls.frontier_out = nf_new;
             ls.mf_in = mf;
-            ls.unvisited_in = nv - visited - ws->n_dead;
+            ls.unvisited_in = nv - visited - n_pre;
             ls.scanned = ws->h_pub->sc;
             ls.claims = ws->h_pub->cl;
             g->level_stats.push_back(ls);
@@ -2941,7 +3110,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                     ls.frontier_in = nf;
                     ls.frontier_out = (int64_t)r.qtail;
                     ls.mf_in = (int64_t)r.scanned;
-                    ls.unvisited_in = nv - visited - ws->n_dead;
+                    ls.unvisited_in = nv - visited - n_pre;
                     ls.scanned = (int64_t)r.scanned;
                     ls.claims = (int64_t)r.claims;
                     g->level_stats.push_back(ls);
@@ -2978,7 +3147,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             td_levels++;
         } else {
             // few unvisited candidates (the tail levels): the sparse kernel, which also queues its discoveries
-            sparse = opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - ws->n_dead) * opt.bu_sparse <= nwords * 64;
+            sparse = opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - n_pre) * opt.bu_sparse <= nwords * 64;
             if (sparse) {
                 const uint32_t qlim = (uint32_t)(opt.leaf_skip ? std::min<int64_t>(ws->leaf_lo, nv) : nv);
                 if (int e = launch_bu_sparse(g, ws, level, qlim, ws->d_pub, ++ws->pub_seq)) return e;
@@ -3006,7 +3175,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         ls.frontier_in = nf;
         ls.frontier_out = nf_new;
         ls.mf_in = (dir == BFSX_DIR_TOPDOWN) ? s.sc : mf; // top-down: the kernels count the rows they sweep
-        ls.unvisited_in = nv - visited - ws->n_dead;      // live candidates (isolated ones are pre-visited)
+        ls.unvisited_in = nv - visited - n_pre;      // live candidates (isolated ones are pre-visited)
         ls.scanned = s.sc;
         ls.claims = s.cl;
         ls.stage2 = s.s2;
@@ -3035,18 +3204,31 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         }
         if (nf == 0) break;
     }
-    // unvisited (non-isolated) vertices -> WHITE; inside the timed region
-    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis, nwords,
-                       ws->st);
+    // unvisited (non-isolated) vertices -> WHITE, deferred degree-1 vertices resolved; inside the timed region
+    {
+        const unsigned wb = clamp_grid((nwords + kBS - 1) / kBS, cap);
+        const int64_t nleaf = defer ? ws->n_def : 0; // the sorted table's valid prefix
+        const int64_t per = (int64_t)kBS * kLeafItems;
+        hipLaunchKernelGGL(k_finalize, dim3(wb + (unsigned)((nleaf + per - 1) / per)), dim3(kBS), 0, st, ws->vis,
+                           nwords, ws->st, wb, ws->lt_p, ws->lt_v, nleaf, ws->leaf_lo, (uint32_t)source,
+                           (uint32_t)level + 1u, ws->d_leafmax);
+    }
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
+    u64 leafmax = 0;
+    if (defer) BFSX_HIP_TRY(hipMemcpyAsync(&leafmax, ws->d_leafmax, sizeof(u64), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
+    if (defer) BFSX_HIP_TRY(hipStreamSynchronize(st));
     if (int e = check_queue_guard(ws)) return e;
-    const int levels = level + 1;
+    const int core_levels = level + 1;
+    // a deferred vertex can sit one level beyond the core's deepest (the last pass expanded distance `level`
+    // and found nothing): the full BFS then has one more pass, which reached only deferred vertices (a
+    // record without kernels); k_finalize flags it
+    const int levels = core_levels + (leafmax ? 1 : 0);
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
     g->level_cum_ms.resize(levels);
-    for (int l = 0; l < levels; l++) {
+    for (int l = 0; l < core_levels; l++) {
         float t = 0.f, k = 0.f;
         const LevelTiming &lt = timing[l];
         if (lt.persisted) { // device clock inside the launch that started at event slot lt.ev
@@ -3060,6 +3242,15 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         g->level_cum_ms[l] = t;
         g->level_stats[l].cum_ms = t;
         g->level_stats[l].kernel_ms = k;
+    }
+    if (levels > core_levels) {
+        bfsx_level_stat ls{};
+        ls.direction = BFSX_DIR_LEAVES;
+        ls.level = core_levels;
+        ls.cum_ms = ms;
+        g->level_stats.push_back(ls);
+        g->level_dirs.push_back(BFSX_DIR_LEAVES);
+        g->level_cum_ms[core_levels] = ms;
     }
     g->last_source = source;
     g->last_t_bfs_ms = ms;
@@ -3374,8 +3565,11 @@ int dist_finish(bfsx_graph *g) {
     if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
     hipStream_t st = g->ctx->stream;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
-    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis,
-                       ws->nwords, ws->st);
+    {
+        const unsigned wb = clamp_grid((ws->nwords + kBS - 1) / kBS, cap);
+        hipLaunchKernelGGL(k_finalize, dim3(wb), dim3(kBS), 0, st, ws->vis, ws->nwords, ws->st, wb, nullptr, nullptr,
+                           (int64_t)0, (int64_t)0, 0u, 0u, nullptr); // no deferred tail
+    }
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
@@ -3647,10 +3841,9 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 slot = std::max<int64_t>(mf, 1);
                 if (int e = grow(ws, ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
                 if (int e = grow(ws, ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
+                // dcount is unused by the slot exchange: its first word counts the workgroups' arrivals
                 hipLaunchKernelGGL(k_bucket_slots, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                                   (uint32_t)g->chunk, (u64)slot, dcursor, ws->sendbuf);
-                BFSX_LAUNCHED(st);
-                hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, st, dcursor, P, (u64)slot, ws->sendbuf);
+                                   (uint32_t)g->chunk, (u64)slot, dcursor, ws->sendbuf, P, dcount);
                 BFSX_LAUNCHED(st);
                 plan_slots(P, slot, plan);
                 ro = P * slot; // candidate entries the claim kernel reads

@@ -51,6 +51,9 @@ extern "C" {
 #define BFSX_DIR_HYBRID 3   /* (level records only) pull from the frontier's hubs + push from its other vertices */
 #define BFSX_DIR_BOTTOMUP_SPARSE 4 /* (level records only) a pull level with few unvisited candidates, run by the
                                      * sparse pull kernel (which also queues the next push frontier) */
+#define BFSX_DIR_LEAVES 5 /* (level records only) the pass that reaches only deferred degree-1 vertices (option
+                           * leaf_defer): they are resolved from their one neighbour after the core levels, so
+                           * this record carries no kernels of its own */
 
 typedef struct bfsx_ctx bfsx_ctx;
 typedef struct bfsx_graph bfsx_graph;
@@ -127,6 +130,14 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device)
  *   "leaf_skip" = on|off (single device: the degree-1 vertices a pull level discovers stay out of the next
  *                 push level's queue -- their one neighbour is their parent; default on)
+ *   "leaf_defer" = on|off (single device: the degree-1 tail of a graph's id space -- on a relabelled graph
+ *                 the ids >= 1 + the last row with two or more entries -- stays out of the level loop: it
+ *                 is pre-visited, push levels never claim it and pull levels skip its bitmap words; after the
+ *                 last level each such vertex takes its one neighbour as parent and that neighbour's
+ *                 distance + 1 (inside the timed region).  Distances, parents, the pass count and
+ *                 bfsx_level_times are those of the full BFS; the per-level frontier counts of
+ *                 bfsx_level_stats exclude the deferred vertices, and a final pass that reaches only them is
+ *                 recorded as BFSX_DIR_LEAVES.  Default off)
  *   "big_degree", "big_cap" = int (partitioned graphs: the ids of degree > big_degree, at most big_cap per
  *                 rank, are all-gathered with their degrees at the first BFS, so every rank knows a source's
  *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS) */
@@ -198,8 +209,9 @@ int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap);
  * `check`): dist[source] = 0 and parent[source] = source; every reached v has a parent joined to it by
  * an edge with dist[parent] = dist[v] - 1; unreached vertices have no parent and no reached neighbour;
  * every edge joins vertices whose distances differ by at most one.  A result that passes holds exactly
- * the BFS distances of the graph.  errors = violating vertices (0 = valid), first_bad = smallest
- * violating id (-1 = none), reached / entries = reached vertices / adjacency entries checked (any
+ * the BFS distances of the graph.  errors = violating vertices (0 = valid), first_bad = one violating
+ * vertex in original ids (-1 = none): the smallest violating id of a graph built without the relabel, the
+ * violating vertex of smallest INTERNAL id (degree order) on a relabelled one, reached / entries = reached vertices / adjacency entries checked (any
  * output may be NULL).  Collective on a partitioned graph (all-gathers the distances).  source < 0 =
  * the source of the most recent BFS. */
 int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first_bad, int64_t *reached,

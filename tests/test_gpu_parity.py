@@ -576,6 +576,9 @@ def test_leaf_skip(ctx):
     option on and off, on (a) a graph whose pull level hands a push level a frontier of leaves only
     (the push level's queue is empty and the pass still counts), (b) Kronecker graphs over many roots,
     with and without K3p and hybrid levels."""
+    # the level structure below is the full loop's: the degree-1 tail stays in it (leaf_defer off;
+    # tests/test_gpu_leaf_defer.py covers the deferred tail)
+    ctx.set_option("leaf_defer", "off")
     # (a) s - h - c_i (3,000) ; c_i - leaf_i for i < 1,000 ; 100,000 isolated ids (n/24 above 3,000)
     s, h = 0, 1
     c = 2 + np.arange(3000)
@@ -624,6 +627,7 @@ def test_leaf_skip(ctx):
         ctx.set_option("persist", "on")
         ctx.set_option("hybrid", "auto")
         ctx.set_option("leaf_skip", "on")
+        ctx.set_option("leaf_defer", "off")
 
 
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
