@@ -115,7 +115,6 @@ struct BfsWorkspace {
     // flag (device word: a deferred vertex lies one level beyond the core's deepest, set by k_finalize)
     u64 *dlf = nullptr;
     int64_t n_def = 0, leaf_hi = 0;
-    uint32_t *lt_p = nullptr, *lt_v = nullptr; // the deferred vertices (lt_v) sorted by their one neighbour (lt_p)
     uint32_t defer_lo = 0;
     u64 *d_leafmax = nullptr;
     // every id >= hub_row_lim has at most hub_deg adjacency entries (the id of the last row with more, + 1;
@@ -1933,9 +1932,9 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const u64 *__restrict__
 // (a grid-stride loop over it ran ~80 dependent iterations per thread: 250 us at scale 26).
 constexpr int kLeafItems = 8;
 __global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ stt,
-                                                  unsigned wblocks, const uint32_t *__restrict__ lt_p,
-                                                  const uint32_t *__restrict__ lt_v, int64_t n_lt, int64_t leaf_lo,
-                                                  uint32_t src, uint32_t deep_d, u64 *deep) {
+                                                  unsigned wblocks, const uint32_t *__restrict__ top1, uint32_t flag,
+                                                  int64_t leaf_lo, int64_t leaf_hi, uint32_t src, uint32_t deep_d,
+                                                  u64 *deep) {
     if (blockIdx.x < wblocks) {
         for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)wblocks * kBS) {
             u64 u = ~vis[w];
@@ -1947,18 +1946,18 @@ __global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, i
         }
         return;
     }
-    // kLeafItems table entries per thread, strided by kBS.  The table (the deferred vertices with their one
-    // neighbour, sorted by that neighbour at workspace creation) is read coalesced and the neighbours' visited
-    // words and states in ascending order, so the gathers walk lines instead of scattering (the deferred
-    // ids themselves, in id order, have their neighbours all over the state array: 150 us at scale 26); the
-    // cost moves to the deferred vertices' own 8-B state stores, which are fire-and-forget.
-    const int64_t i0 = (int64_t)(blockIdx.x - wblocks) * kBS * kLeafItems + threadIdx.x;
+    // kLeafItems deferred ids per thread, strided by kBS (coalesced top1 loads and state stores), every
+    // dependent load issued for all of them before the next: top1 -> {neighbour's visited word, neighbour's
+    // state}.  A self-loop-only row's top1 is itself (>= leaf_lo): WHITE, no loads.  The neighbours' states
+    // are gathered from all over the state array (one line per deferred vertex): that gather is what the
+    // pass costs.
+    const int64_t i0 = leaf_lo + (int64_t)(blockIdx.x - wblocks) * kBS * kLeafItems + threadIdx.x;
     uint32_t p[kLeafItems], v[kLeafItems];
 #pragma unroll
     for (int k = 0; k < kLeafItems; k++) {
-        const int64_t i = i0 + (int64_t)k * kBS;
-        p[k] = i < n_lt ? lt_p[i] : 0xFFFFFFFFu;
-        v[k] = i < n_lt ? lt_v[i] : 0xFFFFFFFFu;
+        const int64_t x = i0 + (int64_t)k * kBS;
+        v[k] = x < leaf_hi ? (uint32_t)x : 0xFFFFFFFFu;
+        p[k] = x < leaf_hi ? top1[x] & ~flag : 0xFFFFFFFFu;
     }
     u64 vw[kLeafItems], sp[kLeafItems];
 #pragma unroll
@@ -1988,16 +1987,6 @@ __global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, i
     // 1.5 ms at scale 26)
     const u64 dm = __ballot(is_deep);
     if (dm && (int)lane_id() == __ffsll((long long)dm) - 1) *deep = 1ull;
-}
-
-// leaf table keys: the one neighbour of every deferred vertex (~0 for a self-loop-only row: not a leaf)
-__global__ __launch_bounds__(kBS) void k_leaf_keys(const uint32_t *__restrict__ top1, uint32_t flag, int64_t lo,
-                                                   int64_t n, uint32_t *__restrict__ key, uint32_t *__restrict__ val) {
-    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
-        const uint32_t v = (uint32_t)(lo + i), p = top1[lo + i] & ~flag;
-        key[i] = p == v ? 0xFFFFFFFFu : p;
-        val[i] = v;
-    }
 }
 
 // 1 + the largest id whose row holds an entry other than itself (the end of the deferred range)
@@ -2454,30 +2443,6 @@ int ws_alloc(bfsx_graph *g) {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
         ws->n_def = (int64_t)nl[0] - (int64_t)nd[0]; // the deferred (non-isolated) vertices
         ws->leaf_hi = std::max<int64_t>(std::min<int64_t>((int64_t)nl[1], g->nv), ws->leaf_lo);
-        // the leaf table: (neighbour, vertex) of every deferred vertex, sorted by neighbour (k_finalize)
-        const int64_t nr = ws->leaf_hi - ws->leaf_lo;
-        if (nr > 0) {
-            struct Tmp {
-                void *p = nullptr;
-                ~Tmp() {
-                    if (p) (void)hipFree(p);
-                }
-            } k1, v1, tmp;
-            BFSX_HIP_TRY(hipMalloc(&k1.p, nr * sizeof(uint32_t)));
-            BFSX_HIP_TRY(hipMalloc(&v1.p, nr * sizeof(uint32_t)));
-            BFSX_HIP_TRY(hipMalloc(&ws->lt_p, nr * sizeof(uint32_t)));
-            BFSX_HIP_TRY(hipMalloc(&ws->lt_v, nr * sizeof(uint32_t)));
-            hipLaunchKernelGGL(k_leaf_keys, dim3(clamp_grid((nr + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->top1,
-                               ws->top1_flag, ws->leaf_lo, nr, (uint32_t *)k1.p, (uint32_t *)v1.p);
-            BFSX_LAUNCHED(st);
-            size_t tb = 0;
-            BFSX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)k1.p, ws->lt_p, (uint32_t *)v1.p, ws->lt_v,
-                                                   (size_t)nr, 0, 32, st));
-            BFSX_HIP_TRY(hipMalloc(&tmp.p, std::max<size_t>(tb, 16)));
-            BFSX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tb, (uint32_t *)k1.p, ws->lt_p, (uint32_t *)v1.p, ws->lt_v,
-                                                   (size_t)nr, 0, 32, st));
-            BFSX_HIP_TRY(hipStreamSynchronize(st)); // the temporaries are freed at the end of this scope
-        }
     }
     return BFSX_OK;
 }
@@ -2868,7 +2833,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr, (void *)ws->out_dist, (void *)ws->out_par, (void *)ws->dlf,
-                    (void *)ws->d_leafmax, (void *)ws->lt_p, (void *)ws->lt_v})
+                    (void *)ws->d_leafmax})
         if (p) (void)hipFree(p);
     for (void *p : ws->retired) (void)hipFree(p);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
@@ -3207,11 +3172,11 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // unvisited (non-isolated) vertices -> WHITE, deferred degree-1 vertices resolved; inside the timed region
     {
         const unsigned wb = clamp_grid((nwords + kBS - 1) / kBS, cap);
-        const int64_t nleaf = defer ? ws->n_def : 0; // the sorted table's valid prefix
+        const int64_t nleaf = defer ? ws->leaf_hi - ws->leaf_lo : 0;
         const int64_t per = (int64_t)kBS * kLeafItems;
         hipLaunchKernelGGL(k_finalize, dim3(wb + (unsigned)((nleaf + per - 1) / per)), dim3(kBS), 0, st, ws->vis,
-                           nwords, ws->st, wb, ws->lt_p, ws->lt_v, nleaf, ws->leaf_lo, (uint32_t)source,
-                           (uint32_t)level + 1u, ws->d_leafmax);
+                           nwords, ws->st, wb, ws->top1, ws->top1_flag, ws->leaf_lo, ws->leaf_lo + nleaf,
+                           (uint32_t)source, (uint32_t)level + 1u, ws->d_leafmax);
     }
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
@@ -3567,7 +3532,7 @@ int dist_finish(bfsx_graph *g) {
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     {
         const unsigned wb = clamp_grid((ws->nwords + kBS - 1) / kBS, cap);
-        hipLaunchKernelGGL(k_finalize, dim3(wb), dim3(kBS), 0, st, ws->vis, ws->nwords, ws->st, wb, nullptr, nullptr,
+        hipLaunchKernelGGL(k_finalize, dim3(wb), dim3(kBS), 0, st, ws->vis, ws->nwords, ws->st, wb, ws->top1, 0u,
                            (int64_t)0, (int64_t)0, 0u, 0u, nullptr); // no deferred tail
     }
     BFSX_LAUNCHED(st);
