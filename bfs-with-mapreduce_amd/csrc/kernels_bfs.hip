@@ -425,7 +425,14 @@ struct Part {
     u64 *remote_tail; // their allocation cursor
     u64 *err;         // mapped host word: set when a queue holds an id >= nrows (null: unchecked)
     uint32_t defer_lo; // option leaf_defer: ids >= defer_lo are never claimed by a push (0: none)
-    uint32_t pad2;
+    uint32_t nranks;
+    // small partitioned push levels (fixed-slot exchange): remote pairs go straight into the send buffer's
+    // per-destination slots [count, slot_cap pairs] (slot_cap 0: into `remote` for the counted exchange);
+    // the level's last push kernel has slot_arrive set: its last workgroup writes the slot counts
+    u64 *slot_out;
+    u64 slot_cap;
+    u64 *slot_cursor;
+    u64 *slot_arrive;
 };
 __device__ inline bool deferred(uint32_t v, uint32_t defer_lo) { return defer_lo && v >= defer_lo; }
 
@@ -442,10 +449,13 @@ __device__ inline bool id_ok(uint32_t u, uint32_t nrows, u64 *err) {
 
 // Remote pairs, LDS-buffered like the local queue (multi-GPU path only).
 constexpr int kRCap = 1024;
+constexpr int kMaxRanks = 64;
 struct RemoteQueue {
     u64 buf[kRCap];
     u64 gbase; // 64-bit: a forced top-down level at scale 30 can route more than 2^32 pairs
     uint32_t n;
+    uint32_t h[kMaxRanks]; // slot mode: this flush's pairs per destination, then their slot bases
+    u64 base[kMaxRanks];
 };
 
 __device__ inline void rq_push(RemoteQueue &q, bool send, u64 pair) {
@@ -462,6 +472,33 @@ __device__ inline void rq_push(RemoteQueue &q, bool send, u64 pair) {
 __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
     const uint32_t n = q.n;
     if (n == 0) return;
+    if (pt.slot_cap) {
+        // fixed-slot exchange: an LDS histogram by destination, ONE reservation atomic per (workgroup,
+        // destination) on the slot cursors, then every pair to its slot (no separate bucketing pass)
+        constexpr int kPer = kRCap / kBS;
+        for (int d = threadIdx.x; d < kMaxRanks; d += kBS) q.h[d] = 0u;
+        __syncthreads();
+        uint32_t r[kPer], dst[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + (uint32_t)k * kBS;
+            dst[k] = i < n ? (uint32_t)(q.buf[i] >> 32) / pt.chunk : 0u;
+            r[k] = i < n ? atomicAdd(&q.h[dst[k]], 1u) : 0u;
+        }
+        __syncthreads();
+        for (int d = threadIdx.x; d < kMaxRanks; d += kBS)
+            if (q.h[d]) q.base[d] = atomicAdd(&pt.slot_cursor[d], (u64)q.h[d]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + (uint32_t)k * kBS;
+            if (i < n) pt.slot_out[(u64)dst[k] * (pt.slot_cap + 1) + 1 + q.base[dst[k]] + r[k]] = q.buf[i];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) q.n = 0;
+        __syncthreads();
+        return;
+    }
     if (threadIdx.x == 0) q.gbase = atomicAdd(pt.remote_tail, (u64)n);
     __syncthreads();
     const u64 gb = q.gbase;
@@ -469,6 +506,24 @@ __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
     __syncthreads();
     if (threadIdx.x == 0) q.n = 0;
     __syncthreads();
+}
+
+// Slot mode, the level's last push kernel: the last workgroup to arrive writes every destination's pair
+// count into its slot header (the cursors are device-scope atomics whose values have all returned:
+// fence-free hand-off as in publish_if_last).  Block-uniform.
+__device__ inline void slot_headers_if_last(const Part &pt) {
+    if (!pt.slot_arrive) return;
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(pt.slot_arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 gridDim.x - 1ull;
+    __syncthreads();
+    if (!s_last) return;
+    for (uint32_t p = threadIdx.x; p < pt.nranks; p += kBS)
+        pt.slot_out[(u64)p * (pt.slot_cap + 1)] =
+            __hip_atomic_load(&pt.slot_cursor[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries; u = local row id)
@@ -599,6 +654,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     // top-down: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
     publish_if_last(cn, pub, seq);
+    if (kDist) slot_headers_if_last(pt);
 }
 
 template <bool kDist, class OffT>
@@ -670,6 +726,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
     publish_if_last(cn, pub, seq);
+    if (kDist) slot_headers_if_last(pt);
 }
 
 // ---- K3p: persistent top-down for narrow frontiers --------------------------------------------------
@@ -1136,13 +1193,46 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
 }
 
+// Multi-GPU level close (k_level_sums below, or the last workgroup of k_claim_remote): the level's counter
+// shards summed into out[0..6] = local {n_f, m_f, m_u, scanned, rows/claims, stage2, walked}, out[8..10] = copy
+// of {n_f, m_f, m_u} (all-reduced in place), and the next level's exchange counters `ctr` zeroed.
+//   out[7] = local d_max of the produced frontier (top-down), out[11] = local vertices found below hub_row_lim
+//   (bottom-up): either tells the next push level whether it needs the hub bin.
+// One wave (threads 0..63) of the calling workgroup; the shards are read with agent-scope loads, so a
+// last-arriving workgroup of the level's last kernel can run it (k_claim_remote) as well as k_level_sums.
+__device__ inline void level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
+                                  u64 *__restrict__ ctr, int nctr) {
+    if (threadIdx.x >= 64) return;
+    const unsigned lane = threadIdx.x;
+    auto ld = [](const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // top-down: the pairs this rank shipped = the sum of the per-destination cursors (slot or counted
+    // exchange), read before the counters are zeroed; recorded as the level's `walked`
+    const u64 shipped = (topdown && nctr >= 1 + 2 * kMaxRanks) ? wave_sum(ld(ctr + 1 + kMaxRanks + lane)) : 0ull;
+    for (int i = lane; i < nctr; i += 64) ctr[i] = 0ull;
+    const StatShard &sh = slot->sh[lane];
+    u64 t[7] = {wave_sum(ld(&sh.nf)),      wave_sum(ld(&sh.mf)),     wave_sum(ld(&sh.mu)),
+                wave_sum(ld(&sh.scanned)), wave_sum(ld(&sh.claims)), wave_sum(ld(&sh.stage2)),
+                wave_sum(ld(&sh.walked))};
+    const u64 dmax = wave_max(ld(&sh.dmax)), nhub = wave_sum(ld(&sh.nhub));
+    if (topdown) {
+        t[0] = ld(&slot->qtail);
+        t[6] = shipped;
+    }
+    if (lane == 0) {
+        for (int i = 0; i < 7; i++) out[i] = (int64_t)t[i];
+        for (int i = 0; i < 3; i++) out[8 + i] = (int64_t)t[i];
+        out[7] = (int64_t)dmax;
+        out[11] = (int64_t)nhub;
+    }
+}
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
 template <class OffT>
 __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pairs, u64 npairs,
                                                       const OffT *__restrict__ row_off, u64 *vis,
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
                                                       LevelSlot *ring, int level, uint32_t lo, u64 slot,
-                                                      uint32_t nrows, u64 *err) {
+                                                      uint32_t nrows, u64 *err, int64_t *sums, u64 *ctr, int nctr,
+                                                      u64 *arrive) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ BlockQueue q;
     bq_init(q);
@@ -1179,14 +1269,23 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     }
     bq_flush(q, qout, &cn->qtail);
     shard_add(cn, 0, acc_mf, 0, attempts, 0, acc_dmax);
+    if (!sums) return;
+    // the level close in the last workgroup to arrive (no k_level_sums dispatch): every wave's queue and
+    // shard atomics have returned or drained before the one agent-scope arrival add
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
+    __syncthreads();
+    if (s_last) level_sums(cn, 1, sums, ctr, nctr);
 }
 
 // Multi-GPU: stable bucketing of remote pairs by owning rank (P <= kMaxRanks).  Two passes over the
 // pairs: per-workgroup destination histograms (LDS atomics), then one reservation atomic per
 // (workgroup, destination) and LDS-ranked scatter.
-constexpr int kMaxRanks = 64;
-// multi-GPU counter block: [0] remote tail | count[64] | cursor[64] | recv count[64] | level sums[16]
-constexpr int kCtrHead = 1 + 2 * kMaxRanks; // zeroed per top-down level
+// multi-GPU counter block: [0] remote tail | count[64] | cursor[64] | arrivals | recv count[64] | level sums[16]
+constexpr int kCtrHead = 2 + 2 * kMaxRanks; // zeroed per level (the last word: k_claim_remote's arrivals)
 constexpr int kCtrRecv = kCtrHead;
 constexpr int kCtrSums = kCtrHead + kMaxRanks;
 constexpr int kCtrWords = kCtrSums + 16;
@@ -1205,33 +1304,9 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pa
         if (s_h[d]) atomicAdd(&dcount[d], (u64)s_h[d]);
 }
 
-// Small top-down levels: pairs go to fixed per-destination slots of [count, cap pairs], so the exchange
-// needs no count all-to-all (and no host round trip) before the pairs move.
-// The slot headers (each destination's pair count) are written by the LAST workgroup to arrive on
-// `arrive` (a zeroed exchange counter), after every workgroup's cursor atomics have returned -- the round-2
-// separate k_slot_headers dispatch is gone (same fence-free hand-off as publish_if_last: the cursors are
-// device-scope atomics, read back with agent-scope loads).
-__global__ __launch_bounds__(kBS) void k_bucket_slots(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
-                                                      uint32_t chunk, u64 cap, u64 *__restrict__ dcursor,
-                                                      u64 *__restrict__ out, int nranks, u64 *arrive) {
-    const uint64_t n = *d_n;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS) {
-        const u64 pr = pairs[i];
-        const uint32_t d = (uint32_t)(pr >> 32) / chunk;
-        const u64 r = atomicAdd(&dcursor[d], 1ull);
-        out[(u64)d * (cap + 1) + 1 + r] = pr;
-    }
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
-    __syncthreads();
-    if (!s_last) return;
-    for (int p = threadIdx.x; p < nranks; p += kBS)
-        out[(u64)p * (cap + 1)] = __hip_atomic_load(&dcursor[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
+// Small top-down levels (fixed per-destination slots of [count, cap pairs], so the exchange needs no count
+// all-to-all and no host round trip before the pairs move) are bucketed by the push kernels themselves
+// (rq_flush in slot mode, slot_headers_if_last); the counted exchange below buckets in two passes.
 __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
                                                         uint32_t chunk, int nranks, const u64 *__restrict__ dcount,
                                                         u64 *__restrict__ dcursor, u64 *__restrict__ out) {
@@ -2208,26 +2283,7 @@ __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict_
 // next top-down level's exchange counters `ctr` (nothing reads them after this level's claim kernel).
 __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
                              u64 *__restrict__ ctr, int nctr) {
-    for (int i = threadIdx.x; i < nctr; i += blockDim.x) ctr[i] = 0ull;
-    constexpr int kSums = 7;
-    __shared__ u64 s[kSums][kShards];
-    for (int i = threadIdx.x; i < kShards; i += blockDim.x) {
-        s[0][i] = slot->sh[i].nf;
-        s[1][i] = slot->sh[i].mf;
-        s[2][i] = slot->sh[i].mu;
-        s[3][i] = slot->sh[i].scanned;
-        s[4][i] = slot->sh[i].claims;
-        s[5][i] = slot->sh[i].stage2;
-        s[6][i] = slot->sh[i].walked;
-    }
-    __syncthreads();
-    if (threadIdx.x < kSums) {
-        u64 t = 0;
-        for (int i = 0; i < kShards; i++) t += s[threadIdx.x][i];
-        if (threadIdx.x == 0 && topdown) t = slot->qtail;
-        out[threadIdx.x] = (int64_t)t;
-        if (threadIdx.x < 3) out[8 + threadIdx.x] = (int64_t)t;
-    }
+    level_sums(slot, topdown, out, ctr, nctr);
 }
 
 unsigned clamp_grid(int64_t blocks, unsigned cap) {
@@ -2507,9 +2563,12 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     // hubs: sized by the frontier's degree sum when known (mf < 0: after a bottom-up level)
     const bool hubs = dmax >= 0 ? dmax > (int64_t)hub_deg : (mf < 0 || mf > (int64_t)hub_deg);
     const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
+    // slot mode: only the level's last push kernel writes the slot headers
+    Part pt0 = pt;
+    if (hubs) pt0.slot_arrive = nullptr;
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip,
+                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
                            hubs ? nullptr : pub, seq);
         BFSX_LAUNCHED(st);
         if (hubs) {
@@ -2519,7 +2578,7 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt, gsz, hs, skip,
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
                            hubs ? nullptr : pub, seq);
         BFSX_LAUNCHED(st);
         if (hubs) {
@@ -3309,6 +3368,7 @@ inline Part make_part(bfsx_graph *g, BfsWorkspace *ws) {
     p.remote_tail = ws->d_dist_ctr;
     p.nrows = (uint32_t)g->nv;
     p.err = ws->d_err;
+    p.nranks = (uint32_t)g->nranks;
     return p;
 }
 
@@ -3454,10 +3514,12 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     const dim3 grid(clamp_grid((n + kBS - 1) / kBS, cap));
     if (ws->off32)
         hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, ws->off32, ws->vis,
-                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err);
+                           ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
+                           nullptr, nullptr, 0, nullptr);
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
-                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err);
+                           ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
+                           nullptr, nullptr, 0, nullptr);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
@@ -3672,13 +3734,15 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
 }
 
 // level close: local sums + all-reduce of (n_f, m_f, m_u); returns [0..4] local, [8..10] global
-int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16]) {
+int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16], bool summed) {
     hipStream_t st = g->ctx->stream;
     const int level = ws->d_level;
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
-    hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums,
-                       ws->d_dist_ctr, kCtrHead);
-    BFSX_LAUNCHED(st);
+    if (!summed) {
+        hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums,
+                           ws->d_dist_ctr, kCtrHead);
+        BFSX_LAUNCHED(st);
+    }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3, st)) return e;
     return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 16, nullptr, 0, reinterpret_cast<u64 *>(out));
@@ -3694,6 +3758,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int rc = dist_ws(g);
     if (rc) return rc;
     BfsWorkspace *ws = g->ws;
+    if ((rc = ensure_hub_row_lim(g, ws))) return rc; // pull levels count their discoveries below it
     hipStream_t st = g->ctx->stream;
     const Options &opt = g->ctx->opt;
     const int P = g->nranks;
@@ -3732,6 +3797,10 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     const bool owner = source >= g->v_lo && source < g->v_lo + g->nv;
+    // the local frontier's largest degree (-1: unknown): at most hub_degree means the next push level needs no
+    // hub bin (k_td_hubs is not launched).  After a push level the kernels' d_max; after a pull level
+    // hub_degree when it found no vertex below hub_row_lim (the rows that can exceed hub_degree)
+    int64_t dmax_local = owner ? deg_local : 0;
     // m_u: an unlisted source's degree (<= big_thr of ~10^9 entries) is left in it until the first pull
     // level recounts m_u exactly; it only feeds Beamer's switch
     int64_t nf = 1, prev_nf = 0, mu = ws->nnz_global - std::max<int64_t>(deg, 0), examined = 0;
@@ -3762,6 +3831,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         if (int e = dist_level_events(ws, level)) return e;
         BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
         const bool td = dir == BFSX_DIR_TOPDOWN;
+        bool summed = false; // the level's last kernel already closed the level (k_claim_remote)
         const bool was_snapped = snapped;
         snapped = false;
         if (td) {
@@ -3791,28 +3861,31 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             }
             if (int e = grow(ws, ws->sendbuf, ws->send_cap, need)) return e;
             // the exchange counters are zero: dist_bfs_run zeroes them before the first level, every
-            // level's k_level_sums after its exchange
-            const Part pt = make_part(g, ws);
+            // level's close (k_claim_remote's last workgroup or k_level_sums) after its exchange
+            Part pt = make_part(g, ws);
             static const bool trace_bufs = std::getenv("BFSX_TRACE") != nullptr;
             if (trace_bufs) trace_buffers(g, ws, level);
-            if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, -1, level, pt)) return e;
             u64 *dcount = ws->d_dist_ctr + 1, *dcursor = ws->d_dist_ctr + 1 + kMaxRanks;
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
             const unsigned gbk = clamp_grid((need + kBS - 1) / kBS, 1024);
             int64_t slot = 0, ro = 0; // slot > 0: fixed-slot exchange
             if (mf <= opt.slot_pairs) {
                 // small level: no rank sends more than the global m_f pairs to any peer, so every peer gets
-                // a fixed slot [count, m_f pairs] -- one exchange, no count all-to-all, no host wait
+                // a fixed slot [count, m_f pairs] -- one exchange, no count all-to-all, no host wait.  The push
+                // kernels write the pairs into the slots themselves; the last one's last workgroup writes the
+                // counts (dcount, unused by the slot exchange, counts its arrivals)
                 slot = std::max<int64_t>(mf, 1);
                 if (int e = grow(ws, ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
                 if (int e = grow(ws, ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
-                // dcount is unused by the slot exchange: its first word counts the workgroups' arrivals
-                hipLaunchKernelGGL(k_bucket_slots, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                                   (uint32_t)g->chunk, (u64)slot, dcursor, ws->sendbuf, P, dcount);
-                BFSX_LAUNCHED(st);
+                pt.slot_out = ws->sendbuf;
+                pt.slot_cap = (u64)slot;
+                pt.slot_cursor = dcursor;
+                pt.slot_arrive = dcount;
                 plan_slots(P, slot, plan);
                 ro = P * slot; // candidate entries the claim kernel reads
-            } else {
+            }
+            if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, dmax_local, level, pt)) return e;
+            if (!slot) {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, P, dcount);
                 BFSX_LAUNCHED(st);
@@ -3830,17 +3903,19 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
                                       plan.rcount.data(), plan.rdispl.data(), st))
                 return e;
-            if (ro > 0) {
+            if (ro > 0) { // its last workgroup closes the level (the sums k_level_sums would compute)
                 const dim3 grid(clamp_grid((ro + kBS - 1) / kBS, cap));
+                u64 *arrive = ws->d_dist_ctr + kCtrHead - 1;
                 if (ws->off32)
                     hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (u64)slot, (uint32_t)g->nv, ws->d_err);
+                                       (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive);
                 else
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (u64)slot, (uint32_t)g->nv, ws->d_err);
+                                       (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive);
                 BFSX_LAUNCHED(st);
+                summed = true;
             }
             td_levels++;
         } else {
@@ -3860,7 +3935,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             if (int e = launch_bu<false>(g, ws, ws->fglob, level)) return e; // m_f from m_u (below)
             bu_levels++;
         }
-        if (int e = dist_level_close(g, ws, td, h)) return e;
+        if (int e = dist_level_close(g, ws, td, h, summed)) return e;
         static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
         if (trace)
             fprintf(stderr, "[bfsx] rank %d level %d %s: nf %lld -> %lld (global %lld)\n", g->rank, level,
@@ -3883,6 +3958,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         visited_local += h[0];
         if (td) std::swap(ws->qa, ws->qb);
         else std::swap(ws->front, ws->next);
+        dmax_local = td ? h[7] : (h[11] == 0 ? (int64_t)opt.hub_degree : -1);
         ws->d_dir = dir;
         ws->d_in_queue = td;
         ws->d_nf = h[0];

@@ -85,7 +85,8 @@ typedef struct bfsx_level_stat {
     double kernel_ms;      /* device time of this level's kernels (hipEvents around them) */
     double cum_ms;         /* device time since source init, like the reference's Stopwatch */
     int64_t stage2;        /* bottom-up: candidates that read their 2nd..4th neighbours (16-B rest[] load) */
-    int64_t walked;        /* bottom-up: adjacency entries read from the CSR past the first four (phase B) */
+    int64_t walked;        /* bottom-up: adjacency entries read from the CSR past the first four (phase B);
+                            * top-down on a partitioned graph: (vertex, parent) pairs this rank sent to others */
 } bfsx_level_stat;
 
 /* ---- library / context ---------------------------------------------------------------------- */
