@@ -144,6 +144,10 @@ struct BfsWorkspace {
     void *persist_ctl = nullptr, *h_pout = nullptr, *d_pout = nullptr;
     int persist_grid = 0;       // workgroups (<= one per CU, all co-resident)
     size_t persist_lds = 0;     // dynamic LDS per workgroup (keeps one workgroup per CU)
+    size_t persist_lds_light = 0; // the same for the instantiation without heavy rows
+    // the graph has a row longer than persist_dmax (heavy_thr: the persist_dmax that was checked; -1 none)
+    bool heavy_rows = true;
+    int64_t heavy_thr = -1;
     u64 persist_bar = 0;        // barrier rounds completed on persist_ctl
     bool persist_reset = true;  // persist_ctl must be zeroed before the next launch
     bool persist_off = false;   // K3p cannot run on this device (occupancy check failed)
@@ -823,7 +827,7 @@ constexpr uint32_t kHeavyMax = 1024;
 // One step of K3p's sweep: kBS * kItems edges [x0, x_end) of a segment table (scan / row start / vertex, n
 // rows).  Winners store their state; light ones (<= heavy_deg entries, or a full heavy region) go to the
 // workgroup's segment, heavy ones to its heavy region (see k_td_persist).  Block-uniform.
-template <class OffT>
+template <class OffT, bool kHeavy>
 __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const uint32_t *t_scan, const int64_t *t_beg,
                                              const uint32_t *t_u, int n, const OffT *__restrict__ row_off,
                                              const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
@@ -872,7 +876,7 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
         bool heavy = false;
         if (win) {
             stt[v[k]] = pack_state(pu[k], nd);
-            if (dg > heavy_deg) { // a heavy row: this workgroup's heavy region, if it has room
+            if (kHeavy && dg > heavy_deg) { // a heavy row: this workgroup's heavy region, if it has room
                 const uint32_t hp = atomicAdd(&s_hn, 1u);
                 if (hp < kHeavyPer) {
                     st_sc1(hout + 2 * hp, (u64)r0[k]);
@@ -906,7 +910,9 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
 // (contiguous); seg: 2 parities x G segments of kRegion; brec: 2 parities x G records (kRecWords); hseg: 2
 // parities x G heavy regions of kHeavyPer entries {row start, vertex | degree << 32}; qfinal: the last
 // frontier, contiguous (light entries, then heavy ones).  bar0: barrier rounds completed by earlier launches.
-template <class OffT>
+// kHeavy = false: the instantiation for graphs without a row longer than persist_dmax (no heavy table, no
+// heavy regions): the heavy machinery costs a largeG-class level ~2 us (19.1 vs 17.0 us per level).
+template <class OffT, bool kHeavy>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_td_persist(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                     const uint32_t *__restrict__ q0, uint32_t nf0, uint32_t *seg,
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
@@ -925,9 +931,10 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     __shared__ uint32_t s_wsum[kWaves];
     __shared__ u64 s_red[9][kWaves];
     __shared__ uint32_t s_n, s_hn;
-    __shared__ uint32_t s_hv[kHeavyMax];
-    __shared__ int64_t s_hb[kHeavyMax];
-    __shared__ uint32_t s_hscan[kHeavyMax + 1];
+    constexpr uint32_t kHT = kHeavy ? kHeavyMax : 1u; // the heavy table's LDS (none without heavy rows)
+    __shared__ uint32_t s_hv[kHT];
+    __shared__ int64_t s_hb[kHT];
+    __shared__ uint32_t s_hscan[kHT + 1];
     (void)s_dyn;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const unsigned G = gridDim.x, b = blockIdx.x;
@@ -953,7 +960,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         }
         u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_eh = 0, acc_dmh = 0;
         // this level's heavy table (every workgroup holds all of it)
-        if (nh_in) {
+        if (kHeavy && nh_in) {
             uint32_t d[kHeavyMax / kBS];
             uint32_t local = 0;
 #pragma unroll
@@ -1038,16 +1045,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             if (tid == 0) scanned += total;
             __syncthreads();
             for (uint32_t x0 = 0; x0 < total; x0 += kBS * kItems)
-                persist_step(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout, hout, s_n,
+                persist_step<OffT, kHeavy>(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout, hout, s_n,
                              s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
             __syncthreads();
         }
         // heavy rows: this workgroup's 1/G share of the heavy table's edges
-        if (nh_in) {
+        if (kHeavy && nh_in) {
             const uint32_t xb = (uint32_t)(eh_in * b / G), xe = (uint32_t)(eh_in * (b + 1) / G);
             if (tid == 0) scanned += xe - xb;
             for (uint32_t x0 = xb; x0 < xe; x0 += kBS * kItems)
-                persist_step(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout,
+                persist_step<OffT, kHeavy>(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout,
                              hout, s_n, s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
         }
         // test hook (option "persist_abort_at"): every workgroup takes the abort path at this level, as a
@@ -1112,14 +1119,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             r_sc = ld_sc1(rout + kRecWords * tid + 2);
             r_cl = ld_sc1(rout + kRecWords * tid + 3);
             r_mfh = ld_sc1(rout + kRecWords * tid + 4);
-            const u64 w5 = ld_sc1(rout + kRecWords * tid + 5);
-            r_nh = w5 & 0xFFFFFFFFull;
-            r_dmh = w5 >> 32;
-            r_eh = ld_sc1(rout + kRecWords * tid + 6);
+            if (kHeavy) {
+                const u64 w5 = ld_sc1(rout + kRecWords * tid + 5);
+                r_nh = w5 & 0xFFFFFFFFull;
+                r_dmh = w5 >> 32;
+                r_eh = ld_sc1(rout + kRecWords * tid + 6);
+            }
         }
-        const uint32_t inc = wave_incl_scan((uint32_t)r_n), hinc = wave_incl_scan((uint32_t)r_nh);
+        const uint32_t inc = wave_incl_scan((uint32_t)r_n), hinc = kHeavy ? wave_incl_scan((uint32_t)r_nh) : 0u;
         const u64 smf = wave_sum(r_mf), ssc = wave_sum(r_sc), scl = wave_sum(r_cl), sdm = wave_max(r_dm),
-                  smfh = wave_sum(r_mfh), seh = wave_sum(r_eh), sdmh = wave_max(r_dmh);
+                  smfh = wave_sum(r_mfh), seh = kHeavy ? wave_sum(r_eh) : 0ull, sdmh = kHeavy ? wave_max(r_dmh) : 0ull;
         __shared__ uint32_t s_hw[kWaves];
         __syncthreads(); // s_red / s_wsum reuse
         if (lane == 63) {
@@ -2522,6 +2531,24 @@ int check_queue_guard(BfsWorkspace *ws) {
                                 std::to_string((uint32_t)e) + ", outside the rows of this graph (stale queue entry)");
 }
 
+// ws->heavy_rows for the current persist_dmax option: does any row exceed it (K3p's heavy instantiation)?  One
+// pass over the row offsets, outside any timed region.
+int ensure_heavy_rows(bfsx_graph *g, BfsWorkspace *ws) {
+    const int64_t thr = g->ctx->opt.persist_dmax;
+    if (ws->heavy_thr == thr) return BFSX_OK;
+    hipStream_t st = g->ctx->stream;
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
+    hipLaunchKernelGGL(k_rows_above, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, g->d_row_off,
+                       g->nv, thr, ws->d_red);
+    BFSX_LAUNCHED(st);
+    u64 lim = 0;
+    BFSX_HIP_TRY(hipMemcpyAsync(&lim, ws->d_red, sizeof(lim), hipMemcpyDeviceToHost, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    ws->heavy_rows = lim > 0;
+    ws->heavy_thr = thr;
+    return BFSX_OK;
+}
+
 // ws->hub_row_lim for the current hub_degree option (one pass over the row offsets, outside any timed region).
 int ensure_hub_row_lim(bfsx_graph *g, BfsWorkspace *ws) {
     const uint32_t hd = g->ctx->opt.hub_degree;
@@ -2789,23 +2816,34 @@ int persist_setup(bfsx_graph *g, BfsWorkspace *ws) {
         // more than half a CU's LDS per workgroup: the dispatcher can place only one per CU
         int lds_cu = 0;
         hipFuncAttributes fa{};
-        const void *kfn = ws->off32 ? reinterpret_cast<const void *>(&k_td_persist<uint32_t>)
-                                    : reinterpret_cast<const void *>(&k_td_persist<int64_t>);
+        // both instantiations (with and without heavy rows) get the same padding, sized by the larger static
+        // LDS (the heavy one), so each one's dynamic share is set for its own static size
+        const void *kfh = ws->off32 ? reinterpret_cast<const void *>(&k_td_persist<uint32_t, true>)
+                                    : reinterpret_cast<const void *>(&k_td_persist<int64_t, true>);
+        const void *kfl = ws->off32 ? reinterpret_cast<const void *>(&k_td_persist<uint32_t, false>)
+                                    : reinterpret_cast<const void *>(&k_td_persist<int64_t, false>);
+        hipFuncAttributes fl{};
         if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, g->ctx->device) ==
                 hipSuccess &&
-            hipFuncGetAttributes(&fa, kfn) == hipSuccess && lds_cu > 0) {
+            hipFuncGetAttributes(&fa, kfh) == hipSuccess && hipFuncGetAttributes(&fl, kfl) == hipSuccess && lds_cu > 0) {
             const size_t want = (size_t)lds_cu / 2 + 1024;
             const size_t dyn = want > fa.sharedSizeBytes ? want - fa.sharedSizeBytes : 0;
-            if (dyn && hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) == hipSuccess)
+            const size_t dynl = want > fl.sharedSizeBytes ? want - fl.sharedSizeBytes : 0;
+            if (dyn && dynl && hipFuncSetAttribute(kfh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) == hipSuccess &&
+                hipFuncSetAttribute(kfl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dynl) == hipSuccess) {
                 ws->persist_lds = dyn;
+                ws->persist_lds_light = dynl;
+            }
             (void)hipGetLastError();
         }
         // the grid barrier needs every workgroup resident at once: never launch more than the occupancy
-        // API says fit (one per CU with the LDS padding above)
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBS, ws->persist_lds) != hipSuccess) per_cu = 0;
+        // API says fit for either instantiation (one per CU with the LDS padding above)
+        int per_cu = 0, per_cul = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfh, kBS, ws->persist_lds) != hipSuccess) per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cul, kfl, kBS, ws->persist_lds_light) != hipSuccess)
+            per_cul = 0;
         (void)hipGetLastError();
-        ws->persist_grid = std::min(G, per_cu * g->ctx->num_cus);
+        ws->persist_grid = std::min(G, std::min(per_cu, per_cul) * g->ctx->num_cus);
         if (ws->persist_grid < 1) {
             ws->persist_off = true; // cannot be co-resident: narrow levels stay per-level launches
             return BFSX_OK;
@@ -2852,14 +2890,20 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
     auto *ctl = reinterpret_cast<PersistCtl *>(ws->persist_ctl);
     auto *dout = reinterpret_cast<PersistOut *>(ws->d_pout);
     const dim3 grid(ws->persist_grid);
+    // the heavy instantiation only when a row can be heavy: the graph has rows longer than persist_dmax, or
+    // the source enters as one
+    const bool heavy = h0_deg > 0 || ws->heavy_rows;
+    auto kp32 = heavy ? &k_td_persist<uint32_t, true> : &k_td_persist<uint32_t, false>;
+    auto kp64 = heavy ? &k_td_persist<int64_t, true> : &k_td_persist<int64_t, false>;
+    const size_t lds = heavy ? ws->persist_lds : ws->persist_lds_light;
     if (ws->off32)
-        hipLaunchKernelGGL(k_td_persist<uint32_t>, grid, dim3(kBS), ws->persist_lds, st, ws->off32, g->d_col, ws->qa,
+        hipLaunchKernelGGL(kp32, grid, dim3(kBS), lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
                            (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
     else
-        hipLaunchKernelGGL(k_td_persist<int64_t>, grid, dim3(kBS), ws->persist_lds, st, g->d_row_off, g->d_col, ws->qa,
+        hipLaunchKernelGGL(kp64, grid, dim3(kBS), lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
@@ -2940,6 +2984,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     if (rc) return rc;
     BfsWorkspace *ws = g->ws;
     if ((rc = ensure_hub_row_lim(g, ws))) return rc;
+    if ((rc = ensure_heavy_rows(g, ws))) return rc;
     bfsx_ctx *ctx = g->ctx;
     hipStream_t st = ctx->stream;
     const Options &opt = ctx->opt;

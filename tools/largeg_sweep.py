@@ -1,5 +1,6 @@
 """largeG-class per-level latency (configs[2] stand-in: 1e6-vertex geometric graph, ~560 levels) under option
-settings, one line per setting: python tools/largeg_sweep.py key=v1,v2,... [key2=...]   (on a GPU box)"""
+settings, one line per setting: python tools/largeg_sweep.py key=v1,v2,... [key2=...]   (on a GPU box).
+BFSX_PKG=<dir holding bfsx.py + libbfsx.so> runs another build (A/B against an earlier commit)."""
 import importlib.util
 import json
 import os
@@ -8,7 +9,8 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-spec = importlib.util.spec_from_file_location("bfsx", os.path.join(ROOT, "bfs-with-mapreduce_amd", "bfsx.py"))
+PKG = os.environ.get("BFSX_PKG", os.path.join(ROOT, "bfs-with-mapreduce_amd"))
+spec = importlib.util.spec_from_file_location("bfsx", os.path.join(PKG, "bfsx.py"))
 bfsx = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(bfsx)
 
@@ -37,7 +39,7 @@ with ctx.from_edges(nv, u, v) as g:
                 d, _, st = g.bfs(0, want_parent=False)
                 ts.append(st["t_bfs_ms"])
             ref = d if ref is None else ref
-            print(json.dumps({k: val, "levels": st["levels"], "t_bfs_ms": round(min(ts), 3),
+            print(json.dumps({"pkg": os.path.basename(PKG), k: val, "levels": st["levels"], "t_bfs_ms": round(min(ts), 3),
                               "us_per_level": round(min(ts) * 1e3 / st["levels"], 2), "same": bool(np.array_equal(d, ref)),
                               "persist_retries": st.get("persist_retries")}), flush=True)
         ctx.set_option(k, "auto" if k == "persist_blocks" else vals.split(",")[0])
