@@ -166,10 +166,17 @@ def measured_traffic(kernel="k_bu"):
         if rec.get("kernels_bfs_sha") == sha and names:
             # the instantiation with the most launches (the hybrid levels' hub sweep is a second one)
             k = max((rec["kernels"][n] for n in names), key=lambda x: x.get("launches", 0))
-            out = {"traffic": round(k["traffic_B"] / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
-                   "traffic_source": os.path.relpath(path, ROOT), "fetch_correction": rec.get("fetch_correction")}
+            # per-access-class correction when the summary has it (round 3: profiles/r03k_fetch_calibration.json),
+            # else the blanket wide-read factor (an upper bound: it doubles the scattered reads too)
+            cls = k.get("traffic_class_B")
+            tb = cls if cls else k["traffic_B"]
+            out = {"traffic": round(tb / 1e6, 1), "traffic_raw": round(k["traffic_raw_B"] / 1e6, 1),
+                   "traffic_blanket": round(k["traffic_B"] / 1e6, 1),
+                   "traffic_source": os.path.relpath(path, ROOT),
+                   "traffic_correction": (k.get("traffic_class_basis") if cls else
+                                          f"FETCH_SIZE x {rec.get('fetch_correction')} (blanket) + WRITE_SIZE")}
             if k.get("avg_ms_trace"):  # fabric-side rate of the same launches (rocprof trace durations)
-                out["traffic_GBs"] = round(k["traffic_B"] / (k["avg_ms_trace"] * 1e-3) / 1e9, 1)
+                out["traffic_GBs"] = round(tb / (k["avg_ms_trace"] * 1e-3) / 1e9, 1)
                 out["traffic_frac"] = round(out["traffic_GBs"] / PEAK_HBM_GBS, 4)
             return out
     return {"traffic": None, "traffic_source": "no PMC summary for this kernel source"}
@@ -207,7 +214,7 @@ class LevelAccount:
             "unit": "GB/s",
             "frac": round(ach / PEAK_HBM_GBS, 4),
             "traffic": tr.pop("traffic"),
-            "traffic_unit": "MB per launch (FETCH_SIZE x correction + WRITE_SIZE)",
+            "traffic_unit": "MB per launch (fabric bytes from FETCH_SIZE / WRITE_SIZE, corrected per access class)",
             "algorithmic": round(self.bu_bytes / max(n, 1) / 1e6, 1),
             **tr,
             "launches": n,

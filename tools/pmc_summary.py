@@ -93,6 +93,19 @@ def main():
         alg = S.mean([bench.level_bytes(l, nwords) for l in bu])
         res["k_bu_algorithmic_B_per_launch"] = alg
         res["k_bu_avg_ms_levels"] = S.mean([l["kernel_ms"] for l in bu])
+        # Per-access-class correction (profiles/r03k_fetch_calibration.json: FETCH_SIZE reads wide coalesced
+        # loads at 1/2 -- 128-B requests tallied at 64 B -- and scattered 4/8/16-B loads at 1/1).  k_bu's wide
+        # class is the visited-word read (one 512-B load per wave: 8 B per 64 vertices) and the top1 loads of
+        # the lane-dense candidate lists (4 B per live candidate); everything else it reads is scattered
+        # (rest[], row offsets and entries, frontier probes, the few scattered top1 lines).  So the fabric read
+        # bytes = raw + wide/2, with wide taken at its algorithmic size; writes are read as counted.
+        wide = S.mean([8 * nwords + 4 * max(l["unvisited_in"], 0) for l in bu])
+        res["k_bu_wide_read_B_per_launch"] = wide
+        for name, k in res["kernels"].items():
+            if name.startswith("k_bu<") and ", false, false, 4, false, true>" in name:
+                k["traffic_class_B"] = k["fetch_raw_B"] + wide / 2 + k["write_B"]
+                k["traffic_class_basis"] = ("FETCH_SIZE raw + the wide-coalesced class (visited words + top1 of "
+                                            "the candidate lists, at algorithmic size) / 2 + WRITE_SIZE")
     except (OSError, KeyError, ValueError, S.StatisticsError):
         pass
     with open(os.path.join(prof, f"{tag}_hbm.json"), "w") as fo:
