@@ -69,7 +69,13 @@ def main():
     corr = 2.0
     if "k_finalize" in fetch and nwords:
         corr = round((8.0 * nwords) / S.mean(fetch["k_finalize"]), 3)
-    res = {"tag": tag, "kernels_bfs_sha": src_hash(), "fetch_correction": corr,
+    # the source the counters were measured on: recorded by the profiling script on the box (src_sha), else
+    # the working tree's (summarise right after the run, before editing the kernels)
+    try:
+        sha = open(os.path.join(d, "src_sha")).read().split()[0][:16]
+    except OSError:
+        sha = src_hash()
+    res = {"tag": tag, "kernels_bfs_sha": sha, "fetch_correction": corr,
            "fetch_correction_basis": "k_finalize reads exactly 8*nwords B (8 B/lane coalesced)"
            if "k_finalize" in fetch else "guide default (x2 for wide streaming reads)",
            "kernels": {}}
