@@ -57,7 +57,7 @@ struct Options {
     int hybrid_pct = 125;       // auto: hybrid when the frontier's hub edges exceed this % of the unvisited count
     int64_t build_chunk = (int64_t)1 << 30; // CSR build: raw adjacency entries per sort/dedup chunk
     int persist_abort_at = -1;  // test hook: K3p aborts at this level of its launch (-1: never)
-    int64_t persist_dmax = 2048; // K3p: longer rows are heavy (swept by the whole grid); a host frontier holding one stays out
+    int64_t persist_dmax = 512; // K3p: longer rows are heavy (swept by the whole grid); a host frontier holding one stays out
     bool poison_queues = false; // test hook: fill the frontier queues and hub list with 0xFF before every BFS
     bool bu_force_spill = false; // diagnostic: the partitioned pull kernel in a spilling (8 waves/SIMD) build
     int test_overread = -1;     // test hook: that top-down level's kernels read one queue entry past the tail

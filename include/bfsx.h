@@ -107,7 +107,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 that every workgroup is resident; fixed at a graph's first BFS)
  *   "persist_dmax" = int (inside the persistent launch a frontier row longer than this is "heavy": the whole
  *                 grid sweeps it, each workgroup an equal share of its edges; a frontier handed to the launch by
- *                 the host may hold one only if it is the source alone; default 2048)
+ *                 the host may hold one only if it is the source alone; default 512: 1,481-1,489 against
+ *                 1,456-1,470 GTEPS at 2048, interleaved on one box, profiles/r03/r03y_persist_dmax_ab.txt)
  *   "persist_abort_at" = int|off (test hook: that persistent launch aborts at its k-th level as a barrier
  *                 timeout would; the BFS is then re-run without it; default off)
  *   "hub_bits" = auto|off|1..30 (bottom-up probes of the 2^b highest-degree vertices go to a small

@@ -703,5 +703,5 @@ def test_persistent_heavy_rows(ctx, dmax):
                     _, _, st = check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=False)
                     assert st["persist_retries"] == 0
     finally:
-        for k, val in (("persist_dmax", "2048"), ("direction", "auto"), ("poison_queues", "off")):
+        for k, val in (("persist_dmax", "512"), ("direction", "auto"), ("poison_queues", "off")):
             ctx.set_option(k, val)
