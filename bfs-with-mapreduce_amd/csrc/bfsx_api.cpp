@@ -307,6 +307,13 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.persist_abort_at = (int)x;
         return BFSX_OK;
     }
+    if (k == "pull_min_edges") {
+        char *end = nullptr;
+        const long long x = std::strtoll(v.c_str(), &end, 10);
+        if (!end || *end || x < 0) return fail(BFSX_E_ARG, "pull_min_edges must be an edge count >= 0");
+        ctx->opt.pull_min_edges = x;
+        return BFSX_OK;
+    }
     if (k == "persist_dmax") {
         char *end = nullptr;
         const long long x = strtoll(value, &end, 10);

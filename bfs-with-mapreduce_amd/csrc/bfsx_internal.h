@@ -32,7 +32,8 @@ struct Options {
     int direction = BFSX_DIR_AUTO;
     int alpha = 20;             // top-down -> bottom-up when m_f > m_u / alpha (re-tuned on scale 26 with the
                                 // two-stage bottom-up: 20 vs 30 = +2%, within run-to-run noise of 10..45)
-    int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
+    int beta = 24;
+    int64_t pull_min_edges = (int64_t)1 << 16; // push -> pull needs at least this many frontier edges (and n/512)              // bottom-up -> top-down when n_f < n / beta (and shrinking)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
     int persist_blocks = 0;     // K3p workgroups (0: one per CU)

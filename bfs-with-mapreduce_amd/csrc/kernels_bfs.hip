@@ -2782,7 +2782,13 @@ struct LevelTiming {
 // cost -- one pass over the n/64-word visited bitmap -- that the tail of a BFS (a few thousand frontier
 // edges against a few thousand unvisited ones) never recovers: 30-40 us pull levels where a push
 // level takes a few.  So a push level hands over only when its frontier has more than n/512 edges.
-int64_t bu_floor(const BfsWorkspace *ws) { return ws->nwords / 8; }
+// The smallest frontier edge count a push -> pull switch needs: a pull level costs a pass over the n/64-word
+// visited bitmap plus the frontier conversions and their dispatches (60-160 us per level at the tail of a
+// 1 M-vertex high-diameter BFS, against ~13 us for a K3p push level), which a frontier of a few ten thousand
+// edges never recovers.  Option pull_min_edges (default 2^16: largeG stand-in 9.69 -> 7.30 ms; scale 26 keeps n/512).
+int64_t bu_floor(const bfsx_graph *g, const BfsWorkspace *ws) {
+    return std::max<int64_t>(ws->nwords / 8, g->ctx->opt.pull_min_edges);
+}
 
 // K3p geometry: at most one workgroup per CU and at most kBS (every workgroup reads all records).
 int persist_blocks(const bfsx_ctx *ctx) {
@@ -2900,13 +2906,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
         hipLaunchKernelGGL(kp32, grid, dim3(kBS), lds, st, ws->off32, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
+                           hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
                            (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
     else
         hipLaunchKernelGGL(kp64, grid, dim3(kBS), lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
-                           hub_set(ws), bu_floor(ws), opt.persist_abort_at, (u64)opt.persist_dmax,
+                           hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
                            (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
@@ -3041,7 +3047,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     for (;; level++) {
         if (opt.direction == BFSX_DIR_AUTO && level > 0) {
             if (dir == BFSX_DIR_TOPDOWN) {
-                if (mf > mu / std::max(opt.alpha, 1) && mf > bu_floor(ws)) dir = BFSX_DIR_BOTTOMUP;
+                if (mf > mu / std::max(opt.alpha, 1) && mf > bu_floor(g, ws)) dir = BFSX_DIR_BOTTOMUP;
             } else if (nf < nbeta / std::max(opt.beta, 1) && nf < prev_nf) {
                 dir = BFSX_DIR_TOPDOWN;
             }

@@ -105,6 +105,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
  *   "persist_blocks" = auto|int (workgroups of that launch, auto = one per CU, capped by the occupancy API so
  *                 that every workgroup is resident; fixed at a graph's first BFS)
+ *   "pull_min_edges" = int (a push -> pull switch also needs the frontier to hold at least this many edges,
+ *                 besides n/512; default 2^16: a pull level's fixed cost is never recovered below it -- the
+ *                 largeG stand-in's tail levels stay in the persistent push launch, 9.69 -> 7.30 ms)
  *   "persist_dmax" = int (inside the persistent launch a frontier row longer than this is "heavy": the whole
  *                 grid sweeps it, each workgroup an equal share of its edges; a frontier handed to the launch by
  *                 the host may hold one only if it is the source alone; default 512: 1,481-1,489 against

@@ -33,6 +33,10 @@ def bfsx():
 @pytest.fixture(scope="session")
 def ctx(bfsx):
     c = bfsx.Context(0)
+    # The test graphs are small: under the default push -> pull floor (pull_min_edges, 2^16 frontier edges)
+    # most of them would never pull, and the pull kernels would go untested.  The suite keeps round 2's
+    # floor (n/512 alone); tests/test_gpu_parity.py::test_pull_floor_default covers the default.
+    c.set_option("pull_min_edges", "0")
     yield c
     c.close()
 

@@ -705,3 +705,31 @@ def test_persistent_heavy_rows(ctx, dmax):
     finally:
         for k, val in (("persist_dmax", "512"), ("direction", "auto"), ("poison_queues", "off")):
             ctx.set_option(k, val)
+
+
+def test_pull_floor_default(ctx):
+    """The default push -> pull floor (pull_min_edges = 2^16 frontier edges): a small graph's BFS stays push
+    (no pull level at all, K3p runs it), a scale-16 Kronecker BFS still pulls (its frontier passes the floor),
+    and both are bit-exact against the oracle; with the floor at 0 the small graph pulls again."""
+    rng = np.random.default_rng(61)
+    nv = 20000
+    u = rng.integers(0, nv, 3 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 3 * nv).astype(np.uint32)
+    off, col = O.build_sets(nv, u, v)
+    ou, ov = O.kronecker(16, 16, 0x5EED2026)
+    koff, kcol = O.build_sets(1 << 16, ou, ov)
+    try:
+        ctx.set_option("pull_min_edges", "65536")
+        with ctx.from_edges(nv, u, v) as g:
+            check_against_oracle(g, nv, off, col, 0, u, v, mr=False)
+            assert all(d == 1 for d in g.level_dirs())
+        with ctx.kronecker(16, 16, 0x5EED2026) as g:
+            r = int(g.sample_roots(1, seed=2)[0])
+            check_against_oracle(g, 1 << 16, koff, kcol, r, ou, ov, mr=False)
+            assert 2 in list(g.level_dirs())
+        ctx.set_option("pull_min_edges", "0")
+        with ctx.from_edges(nv, u, v) as g:
+            check_against_oracle(g, nv, off, col, 0, u, v, mr=False)
+            assert any(d in (2, 4) for d in g.level_dirs())
+    finally:
+        ctx.set_option("pull_min_edges", "0")

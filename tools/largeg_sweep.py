@@ -39,6 +39,9 @@ with ctx.from_edges(nv, u, v) as g:
                 d, _, st = g.bfs(0, want_parent=False)
                 ts.append(st["t_bfs_ms"])
             ref = d if ref is None else ref
+            if os.environ.get("LEVELS_OUT"):  # per-level records of the last run of this setting
+                with open(f"{os.environ['LEVELS_OUT']}_{k}_{val}.json", "w") as f:
+                    json.dump(g.level_stats(4096), f)
             print(json.dumps({"pkg": os.path.basename(PKG), k: val, "levels": st["levels"], "t_bfs_ms": round(min(ts), 3),
                               "us_per_level": round(min(ts) * 1e3 / st["levels"], 2), "same": bool(np.array_equal(d, ref)),
                               "persist_retries": st.get("persist_retries")}), flush=True)
