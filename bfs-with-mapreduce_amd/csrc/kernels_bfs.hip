@@ -138,7 +138,7 @@ struct BfsWorkspace {
     Published *h_pub = nullptr, *d_pub = nullptr; // mapped pinned level counters (host / device view)
     // K3p (persistent top-down): output segments, workgroup records, barrier state (device) and the
     // launch result (mapped pinned host memory)
-    uint32_t *persist_seg = nullptr;
+    u64 *persist_seg = nullptr;         // K3p segments: 2 parities x G x kRegion entries of 16 B
     u64 *persist_brec = nullptr;
     u64 *persist_hseg = nullptr;        // heavy-row regions: 2 parities x G x kHeavyPer x {row start, v | deg << 32}
     void *persist_ctl = nullptr, *h_pout = nullptr, *d_pout = nullptr;
@@ -831,7 +831,7 @@ template <class OffT, bool kHeavy>
 __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const uint32_t *t_scan, const int64_t *t_beg,
                                              const uint32_t *t_u, int n, const OffT *__restrict__ row_off,
                                              const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                             int32_t nd, HubSet hs, u64 heavy_deg, uint32_t defer_lo, uint32_t *sout,
+                                             int32_t nd, HubSet hs, u64 heavy_deg, uint32_t defer_lo, u64 *sout,
                                              u64 *hout, uint32_t &s_n, uint32_t &s_hn, PersistCtl *ctl, u64 &acc_mf,
                                              u64 &attempts, u64 &acc_dmax, u64 &acc_mfh, u64 &acc_eh, u64 &acc_dmh) {
     const unsigned tid = threadIdx.x, lane = tid & 63u;
@@ -899,7 +899,10 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
             if ((int)lane == leader) pos = atomicAdd(&s_n, (uint32_t)__popcll(mask));
             pos = __shfl(pos, leader) + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
             if (light) {
-                if (pos < kRegion) st_sc1(sout + pos, v[k]);
+                if (pos < kRegion) { // the entry carries its row bounds: the next level needs no row_off load
+                    st_sc1(sout + 2 * pos, (u64)r0[k]);
+                    st_sc1(sout + 2 * pos + 1, (u64)v[k] | (dg << 32));
+                }
                 else st_sc1(&ctl->abort, 1ull); // cannot happen: slices are bounded on entry
             }
         }
@@ -914,7 +917,7 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
 // heavy regions): the heavy machinery costs a largeG-class level ~2 us (19.1 vs 17.0 us per level).
 template <class OffT, bool kHeavy>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_td_persist(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                                    const uint32_t *__restrict__ q0, uint32_t nf0, uint32_t *seg,
+                                                    const uint32_t *__restrict__ q0, uint32_t nf0, u64 *seg,
                                                     u64 *brec, uint32_t *__restrict__ qfinal, u64 *vis,
                                                     u64 *__restrict__ stt, LevelSlot *ring, int level0, int64_t mu0,
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
@@ -948,8 +951,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     u64 eh_in = h0_deg;
     int64_t mu = mu0;
     for (int it = 0;; it++) {
-        const uint32_t *sin = seg + (size_t)((it + 1) & 1) * G * kRegion; // previous level's segments
-        uint32_t *sout = seg + (size_t)(it & 1) * G * kRegion + (size_t)b * kRegion;
+        // segments of 16-B entries {row start, vertex | degree << 32}
+        const u64 *sin = seg + (size_t)((it + 1) & 1) * G * kRegion * 2; // previous level's segments
+        u64 *sout = seg + ((size_t)(it & 1) * G * kRegion + (size_t)b * kRegion) * 2;
         const u64 *hin = hseg + (size_t)((it + 1) & 1) * G * kHeavyPer * 2;   // previous level's heavy regions
         u64 *hout = hseg + ((size_t)(it & 1) * G + b) * kHeavyPer * 2;          // this workgroup's
         u64 *rout = brec + (size_t)(it & 1) * G * kRecWords;
@@ -1020,13 +1024,19 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                         if (s_off[mid] <= i) lo = mid;
                         else hi = mid - 1;
                     }
-                    u = ld_sc1(sin + (size_t)lo * kRegion + (i - s_off[lo]));
+                    const u64 *e = sin + ((size_t)lo * kRegion + (i - s_off[lo])) * 2;
+                    beg = (int64_t)ld_sc1(e);
+                    const u64 w = ld_sc1(e + 1);
+                    u = (uint32_t)w;
+                    deg = (uint32_t)(w >> 32);
                 }
-                if (u != 0xFFFFFFFFu) {
-                    beg = (int64_t)row_off[u];
-                    deg = (uint32_t)((int64_t)row_off[u + 1] - beg);
-                } else {
-                    u = 0; // a rejected q0 entry: an empty row
+                if (it == 0) {
+                    if (u != 0xFFFFFFFFu) {
+                        beg = (int64_t)row_off[u];
+                        deg = (uint32_t)((int64_t)row_off[u + 1] - beg);
+                    } else {
+                        u = 0; // a rejected q0 entry: an empty row
+                    }
                 }
             }
             const uint32_t inc = wave_incl_scan(deg);
@@ -1191,7 +1201,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         __syncthreads();
         if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones
             const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
-            for (uint32_t i = tid; i < nb; i += kBS) qfinal[ob + i] = ld_sc1(sout + i);
+            for (uint32_t i = tid; i < nb; i += kBS) qfinal[ob + i] = (uint32_t)ld_sc1(sout + 2 * i + 1);
             const uint32_t hb = (b + 1 < G ? s_hoff[b + 1] : nh_new) - s_hoff[b], hbase = nf_new + s_hoff[b];
             for (uint32_t i = tid; i < hb; i += kBS) qfinal[hbase + i] = (uint32_t)ld_sc1(hout + 2 * i + 1);
             return;
@@ -2809,7 +2819,7 @@ int persist_setup(bfsx_graph *g, BfsWorkspace *ws) {
     if (!ws->persist_seg) {
         const int G = persist_blocks(g->ctx);
         ws->persist_grid = G;
-        BFSX_HIP_TRY(hipMalloc(&ws->persist_seg, (size_t)2 * G * kRegion * sizeof(uint32_t)));
+        BFSX_HIP_TRY(hipMalloc(&ws->persist_seg, (size_t)2 * G * kRegion * 2 * sizeof(u64)));
         BFSX_HIP_TRY(hipMalloc(&ws->persist_brec, (size_t)2 * G * kRecWords * sizeof(u64)));
         BFSX_HIP_TRY(hipMalloc(&ws->persist_hseg, (size_t)2 * G * kHeavyPer * 2 * sizeof(u64)));
         BFSX_HIP_TRY(hipMalloc(&ws->persist_ctl, sizeof(PersistCtl)));
