@@ -135,6 +135,12 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device)
  *   "leaf_skip" = on|off (single device: the degree-1 vertices a pull level discovers stay out of the next
  *                 push level's queue -- their one neighbour is their parent; default on)
+ *   "relabel" = on|off (graphs built after the call renumber their vertices by degree, descending, inside every
+ *                 rank's id range; results are always in the caller's ids; default on)
+ *   Test hooks and diagnostics (not for production): "poison_queues" = on|off (fill the frontier queues and
+ *                 the hub list with 0xFF before every BFS), "test_overread" = int|off (that push level reads one
+ *                 queue entry past its tail: the id guard must fail the BFS), "bu_force_spill" = on|off (the
+ *                 partitioned pull kernel in a build that spills to scratch)
  *   "leaf_defer" = on|off (single device: the degree-1 tail of a graph's id space -- on a relabelled graph
  *                 the ids >= 1 + the last row with two or more entries -- stays out of the level loop: it
  *                 is pre-visited, push levels never claim it and pull levels skip its bitmap words; after the
