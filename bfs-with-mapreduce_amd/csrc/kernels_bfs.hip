@@ -148,8 +148,8 @@ struct BfsWorkspace {
     // the graph has a row longer than persist_dmax (heavy_thr: the persist_dmax that was checked; -1 none)
     bool heavy_rows = true;
     int64_t heavy_thr = -1;
-    u64 persist_bar = 0;        // barrier rounds completed on persist_ctl
-    bool persist_reset = true;  // persist_ctl must be zeroed before the next launch
+    u64 persist_bar = 0;        // K3p levels run since the records were last zeroed (the record tag base)
+    bool persist_reset = true;  // persist_ctl and the records must be zeroed before the next launch
     bool persist_off = false;   // K3p cannot run on this device (occupancy check failed)
     int64_t persist_fallbacks = 0; // BFS runs re-run without K3p after a barrier abort
     double clock_khz = 100000.0; // device wall-clock rate
@@ -741,30 +741,26 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
 //   * workgroup b takes the frontier slice [nf*b/G, nf*(b+1)/G) and sweeps its rows edge-parallel
 //     (as k_td); the vis word and the target's row offsets are loaded together, so a win costs no
 //     further round trip;
-//   * winners go straight to b's own output segment (kRegion slots; LDS counter, no global cursor),
-//     written through L2 (`sc1` stores), and b's level record {n, m_f, scanned, claims, d_max};
-//   * a grid barrier on 8 sharded arrival counters (one per `blockIdx % 8`); every workgroup then
-//     reads the G records (`sc1` loads), scans the counts into segment offsets and takes the same
+//   * winners go straight to b's own output segment (kRegion slots of {row start, vertex | degree}; LDS
+//     counter, no global cursor), written through L2 (`sc1` stores), and b's level record {n, m_f,
+//     scanned, claims, d_max};
+//   * the records are the grid barrier (round 3): every word carries the level's 16-bit tag, and thread t
+//     of every workgroup polls workgroup t's record until it holds the tag -- so the arrival and the record
+//     read are one round trip (an arrival counter plus a separate record read cost the largeG stand-in
+//     1.5 us per level).  Every workgroup then scans the counts into segment offsets and takes the same
 //     decision: continue, or stop when the BFS ends, the next frontier is no longer narrow (n_f >
 //     kPersistNf, or a slice could hold more than kRegion edges), Beamer's rule asks for bottom-up or
 //     the level budget is used up.  On stop every workgroup copies its segment into the contiguous
 //     queue the per-level kernels read.
 // Hand-off form (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table): every
 // handed-off byte (segment entries, records) is stored `sc1` and loaded `sc1`; every wave waits
-// vmcnt(0) before the workgroup barrier behind which one lane adds to the arrival counter; the poll
-// is an `sc1` load of every shard.  Visited words are claimed by device atomics (a stale plain
+// vmcnt(0) before the workgroup barrier behind which one lane writes the tagged record; the poll is an
+// `sc1` load of every record's tagged words.  Visited words are claimed by device atomics (a stale plain
 // pre-check can only under-report a set bit), the state array is read only after the launch.
 constexpr uint32_t kRegion = 16384; // output slots per workgroup and level parity
-constexpr int kBarShards = 8;
-
-struct alignas(128) BarShard {
-    u64 v;
-    u64 pad[15];
-};
 struct alignas(128) PersistCtl {
-    BarShard arr[kBarShards]; // monotonic across launches (the host passes the rounds already done)
-    u64 abort;
-    u64 pad[7];
+    u64 abort; // raised by a workgroup whose poll timed out or whose segment would overflow
+    u64 pad[15];
 };
 // host-visible result of one launch (mapped pinned memory, written by workgroup 0)
 struct alignas(64) PersistOut {
@@ -772,46 +768,9 @@ struct alignas(64) PersistOut {
     PersistRec rec[kPersistLevels];
 };
 
-__device__ inline void st_sc1(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ inline void st_sc1(u64 *p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ inline uint32_t ld_sc1(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ inline u64 ld_sc1(const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-// Arrive on this workgroup's shard and wait until every shard holds `round` arrivals of each of its
-// workgroups.  Block-uniform; false: a workgroup raised abort (or this one timed out).
-__device__ inline bool grid_sync(PersistCtl *ctl, u64 round) {
-    __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const unsigned l = threadIdx.x, G = gridDim.x;
-        if (l == 0) __hip_atomic_fetch_add(&ctl->arr[blockIdx.x % kBarShards].v, 1ull, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-        const u64 target = l < (unsigned)kBarShards ? round * (u64)((G - l + kBarShards - 1) / kBarShards) : 0ull;
-        int ok = 1;
-        for (uint32_t spin = 0;; spin++) {
-            const u64 x = l < (unsigned)kBarShards ? ld_sc1(&ctl->arr[l].v) : ~0ull;
-            if (__all(x >= target)) break;
-            if (ld_sc1(&ctl->abort)) {
-                ok = 0;
-                break;
-            }
-            if (spin > (1u << 22)) {
-                if (l == 0) st_sc1(&ctl->abort, 1ull);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (l == 0) s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
 
 // Heavy rows inside K3p (round 3).  A frontier vertex with more than `heavy_deg` entries is not swept by the
 // one workgroup whose slice holds it: the workgroup that discovers it records it in its own heavy region
@@ -957,6 +916,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         const u64 *hin = hseg + (size_t)((it + 1) & 1) * G * kHeavyPer * 2;   // previous level's heavy regions
         u64 *hout = hseg + ((size_t)(it & 1) * G + b) * kHeavyPer * 2;          // this workgroup's
         u64 *rout = brec + (size_t)(it & 1) * G * kRecWords;
+        const u64 tag = ((bar0 + (u64)it + 1) & 0xFFFFull) << 48; // this level's record tag (never 0)
         const int32_t nd = level0 + it + 1;
         if (tid == 0) {
             s_n = 0;
@@ -1090,6 +1050,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                 s_red[5][wave] = v5;
                 s_red[6][wave] = v6;
             }
+            // the record is the arrival: every wave's segment / heavy-region / claim traffic must have
+            // completed before thread 0 writes it
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
                 u64 a = 0, c = 0, d = 0, m = 0, h = 0, e = 0, mh = 0;
@@ -1103,37 +1066,79 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                     mh = s_red[6][w] > mh ? s_red[6][w] : mh;
                 }
                 const u64 nh = min(s_hn, kHeavyPer);
-                st_sc1(rout + kRecWords * b + 0, (u64)s_n | (m << 32));
-                st_sc1(rout + kRecWords * b + 1, a);
-                st_sc1(rout + kRecWords * b + 2, c);
-                st_sc1(rout + kRecWords * b + 3, d);
-                st_sc1(rout + kRecWords * b + 4, h);
-                st_sc1(rout + kRecWords * b + 5, nh | (mh << 32));
-                st_sc1(rout + kRecWords * b + 6, e);
+                // every word carries the level's 16-bit tag (bits 48..63): the words are the barrier
+                constexpr u64 k24 = (1ull << 24) - 1, k48 = (1ull << 48) - 1;
+                u64 *r = rout + kRecWords * b;
+                st_sc1(r + 0, (u64)s_n | (min(m, k24) << 24) | tag);
+                st_sc1(r + 1, min(a, k48) | tag);
+                st_sc1(r + 2, min(c, k48) | tag);
+                st_sc1(r + 3, min(d, k48) | tag);
+                st_sc1(r + 4, min(h, k48) | tag);
+                if (kHeavy) {
+                    st_sc1(r + 5, nh | (min(mh, k24) << 24) | tag);
+                    st_sc1(r + 6, min(e, k48) | tag);
+                }
             }
         }
-        if (!grid_sync(ctl, bar0 + (u64)it + 1)) {
-            if (b == 0 && tid == 0) {
-                out->abort = 1;
-                out->levels = (u64)it;
-            }
-            return;
-        }
-        // every workgroup: the G records -> segment and heavy-region offsets and the level's sums
+        // Barrier and record exchange in one: thread t < G polls workgroup t's record until every word
+        // carries this level's tag (no arrival counter, no separate record read after it).  d_max values
+        // are clamped to 2^24 - 1: any value above kRegion stops the launch anyway.
         u64 r_n = 0, r_dm = 0, r_mf = 0, r_sc = 0, r_cl = 0, r_mfh = 0, r_nh = 0, r_dmh = 0, r_eh = 0;
-        if (tid < G) {
-            const u64 w0 = ld_sc1(rout + kRecWords * tid);
-            r_n = w0 & 0xFFFFFFFFull;
-            r_dm = w0 >> 32;
-            r_mf = ld_sc1(rout + kRecWords * tid + 1);
-            r_sc = ld_sc1(rout + kRecWords * tid + 2);
-            r_cl = ld_sc1(rout + kRecWords * tid + 3);
-            r_mfh = ld_sc1(rout + kRecWords * tid + 4);
-            if (kHeavy) {
-                const u64 w5 = ld_sc1(rout + kRecWords * tid + 5);
-                r_nh = w5 & 0xFFFFFFFFull;
-                r_dmh = w5 >> 32;
-                r_eh = ld_sc1(rout + kRecWords * tid + 6);
+        {
+            __shared__ int s_ok;
+            if (tid == 0) s_ok = 1;
+            __syncthreads();
+            constexpr u64 k24 = (1ull << 24) - 1, k48 = (1ull << 48) - 1;
+            const u64 *rr = rout + kRecWords * tid;
+            u64 w[kRecWords] = {0, 0, 0, 0, 0, 0, 0};
+            constexpr int kw = kHeavy ? kRecWords : 5;
+            for (uint32_t spin = 0;; spin++) {
+                // poll the first word alone while waiting (1/kw of the traffic), then the others once
+                bool ok = true;
+                if (tid < G) {
+                    w[0] = ld_sc1(rr);
+                    ok = (w[0] & ~k48) == tag;
+                }
+                if (__all(ok)) {
+                    if (tid < G) {
+#pragma unroll
+                        for (int i = 1; i < kw; i++) w[i] = ld_sc1(rr + i);
+#pragma unroll
+                        for (int i = 1; i < kw; i++) ok = ok && (w[i] & ~k48) == tag;
+                    }
+                    if (__all(ok)) break;
+                }
+                if (ld_sc1(&ctl->abort)) {
+                    s_ok = 0;
+                    break;
+                }
+                if (spin > (1u << 22)) {
+                    if (lane == 0) st_sc1(&ctl->abort, 1ull);
+                    s_ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __syncthreads();
+            if (!s_ok) {
+                if (b == 0 && tid == 0) {
+                    out->abort = 1;
+                    out->levels = (u64)it;
+                }
+                return;
+            }
+            if (tid < G) {
+                r_n = w[0] & k24;
+                r_dm = (w[0] >> 24) & k24;
+                r_mf = w[1] & k48;
+                r_sc = w[2] & k48;
+                r_cl = w[3] & k48;
+                r_mfh = w[4] & k48;
+                if (kHeavy) {
+                    r_nh = w[5] & k24;
+                    r_dmh = (w[5] >> 24) & k24;
+                    r_eh = w[6] & k48;
+                }
             }
         }
         const uint32_t inc = wave_incl_scan((uint32_t)r_n), hinc = kHeavy ? wave_incl_scan((uint32_t)r_nh) : 0u;
@@ -2894,8 +2899,11 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
     hipStream_t st = g->ctx->stream;
     const Options &opt = g->ctx->opt;
     if (!ws->persist_seg || ws->persist_off) return 0; // persist_fits sets K3p up before the first launch
-    if (ws->persist_reset) {
+    // record tags are 16 bits of the monotonic level count: before they could wrap within a launch, and after
+    // an abort, the records are zeroed (tag 0 is never used) and the count restarts
+    if (ws->persist_reset || ws->persist_bar + (u64)kPersistLevels + 1 > 0xFFFFull) {
         BFSX_HIP_TRY(hipMemsetAsync(ws->persist_ctl, 0, sizeof(PersistCtl), st));
+        BFSX_HIP_TRY(hipMemsetAsync(ws->persist_brec, 0, (size_t)2 * ws->persist_grid * kRecWords * sizeof(u64), st));
         ws->persist_bar = 0;
         ws->persist_reset = false;
     }
