@@ -239,6 +239,18 @@ class LevelAccount:
         }
 
 
+def account_levels(acct, g, order, raw, keep):
+    """Decode the level records the timed loop copied (one bytes blob per BFS, g.level_stats_raw) into the
+    byte account; returns every level tagged with its root when `keep` (--levels-json), else []."""
+    kept = []
+    for r, blob in zip(order, raw):
+        lv = g.level_stats_decode(blob)
+        acct.add(lv)
+        if keep:
+            kept.extend(dict(ls, root=r) for ls in lv)
+    return kept
+
+
 def edge_scan_equivalent(m, nv, t_mean_ms):
     b = 8.0 * m + 12.0 * nv
     ach = b / (t_mean_ms * 1e-3) / 1e9
@@ -371,17 +383,15 @@ def run_single(args):
     acct = LevelAccount(nwords, off_bytes)
     ctx.synchronize()
     w0 = time.perf_counter()
-    t_bfs, order, all_levels = [], [], []
+    t_bfs, order, raw = [], [], []
     for _ in range(args.steps):
         for r in roots:
             t_bfs.append(g.bfs_device_only(r))
             order.append(r)
-            lv = g.level_stats(256)
-            acct.add(lv)
-            if args.levels_json:
-                all_levels.extend(dict(ls, root=r) for ls in lv)
+            raw.append(g.level_stats_raw(256))  # decoded after the timed region
     ctx.synchronize()
     wall = time.perf_counter() - w0
+    all_levels = account_levels(acct, g, order, raw, args.levels_json)
 
     gteps = [mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(order, t_bfs)]
     # output conversion (outside t_bfs): the unpack kernel that turns the packed internal-id state into the
@@ -482,18 +492,16 @@ def run_dist(args, world, rank, local_rank):
     ctx.synchronize()
     dist.barrier()
     w0 = time.perf_counter()
-    dev_ms, order, all_levels = [], [], []
+    dev_ms, order, raw = [], [], []
     for _ in range(args.steps):
         for r in roots:
             dev_ms.append(g.dist_bfs(r, want_stats=False))
             order.append(r)
             if rank == 0:
-                lv = g.level_stats(256)
-                acct.add(lv)
-                if args.levels_json:
-                    all_levels.extend(dict(ls, root=r) for ls in lv)
+                raw.append(g.level_stats_raw(256))  # decoded after the timed region
     ctx.synchronize()
     wall_local = time.perf_counter() - w0
+    all_levels = account_levels(acct, g, order, raw, args.levels_json)
     dist.barrier()
     tt = torch.tensor([wall_local] + dev_ms, dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)  # max over ranks

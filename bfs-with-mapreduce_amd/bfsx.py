@@ -419,6 +419,21 @@ class Graph:
         n = lib().bfsx_level_stats(self._h, buf, cap)
         return [{k: getattr(buf[i], k) for k, _ in LevelStat._fields_} for i in range(n)]
 
+    def level_stats_raw(self, cap=256):
+        """The most recent BFS's level records as one bytes copy, with no per-field conversion (a few us, so a
+        timed loop can keep every BFS's records); level_stats_decode turns it into level_stats()'s dicts."""
+        buf = getattr(self, "_ls_buf", None)
+        if buf is None or len(buf) < cap:
+            buf = self._ls_buf = (LevelStat * cap)()
+        n = lib().bfsx_level_stats(self._h, buf, cap)
+        return C.string_at(buf, max(n, 0) * C.sizeof(LevelStat))
+
+    @staticmethod
+    def level_stats_decode(raw):
+        n = len(raw) // C.sizeof(LevelStat)
+        buf = (LevelStat * n).from_buffer_copy(raw) if n else ()
+        return [{k: getattr(buf[i], k) for k, _ in LevelStat._fields_} for i in range(n)]
+
     def free(self):
         if self._h:
             lib().bfsx_graph_free(self._h)

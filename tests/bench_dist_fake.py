@@ -43,6 +43,13 @@ def fake_bfsx():
                     {"level": 1, "direction": 2, "frontier_in": 10, "frontier_out": 0, "mf_in": 0,
                      "kernel_ms": 0.2, "unvisited_in": 50, "stage2": 5, "claims": 1, "walked": 3, "scanned": 60}]
 
+        def level_stats_raw(self, cap=256):
+            return self.level_stats(cap)
+
+        @staticmethod
+        def level_stats_decode(raw):
+            return raw
+
         def free(self):
             pass
 

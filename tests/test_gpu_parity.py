@@ -733,3 +733,15 @@ def test_pull_floor_default(ctx):
             assert any(d in (2, 4) for d in g.level_dirs())
     finally:
         ctx.set_option("pull_min_edges", "0")
+
+
+def test_level_stats_raw_matches(ctx):
+    """bench.py's timed loop copies each BFS's level records raw (level_stats_raw) and decodes them after the
+    timed region: the decoded records must equal level_stats()'s, including a cap below the level count."""
+    with ctx.kronecker(14, 16, 0xA11) as g:
+        for r in [int(x) for x in g.sample_roots(3, seed=5)]:
+            g.bfs_device_only(r)
+            full = g.level_stats()
+            assert len(full) >= 2
+            assert g.level_stats_decode(g.level_stats_raw(256)) == full
+            assert g.level_stats_decode(g.level_stats_raw(1)) == full[:1]
