@@ -48,6 +48,30 @@ def test_level_account_whole_bfs(bench):
     assert bench.edge_scan_equivalent(1 << 20, 1 << 16, 1.0)["frac_of_peak"] > 0
 
 
+def test_account_levels_decodes_raw_records(bench):
+    """The timed loop keeps one raw LevelStat blob per BFS (Graph.level_stats_raw); account_levels decodes them
+    after the region into the same account that the per-BFS dicts would give, keeping roots for --levels-json."""
+    import ctypes as C
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "bfs-with-mapreduce_amd"))
+    from bfsx import Graph, LevelStat
+    recs = [dict(direction=1, frontier_in=10, mf_in=300, frontier_out=20, kernel_ms=0.1),
+            dict(direction=2, unvisited_in=1000, stage2=100, claims=10, walked=1 << 40, frontier_out=600,
+                 kernel_ms=0.5)]
+    buf = (LevelStat * 2)()
+    for i, r in enumerate(recs):
+        for k, v in r.items():
+            setattr(buf[i], k, v)
+    blob = C.string_at(buf, 2 * C.sizeof(LevelStat))
+    a, b = bench.LevelAccount(64, 4), bench.LevelAccount(64, 4)
+    kept = bench.account_levels(a, Graph, [7, 9], [blob, blob[:C.sizeof(LevelStat)]], True)
+    b.add(Graph.level_stats_decode(blob))
+    b.add(Graph.level_stats_decode(blob)[:1])
+    assert (a.all_bytes, a.bu_bytes, a.bu_ms, a.bu_launches) == (b.all_bytes, b.bu_bytes, b.bu_ms, b.bu_launches)
+    assert [k["root"] for k in kept] == [7, 7, 9] and kept[1]["walked"] == 1 << 40
+    assert bench.account_levels(bench.LevelAccount(64, 4), Graph, [7], [b""], False) == []
+
+
 def test_hmean(bench):
     assert bench.hmean([1.0, 1.0]) == 1.0
     assert abs(bench.hmean([1.0, 3.0]) - 1.5) < 1e-12
