@@ -14,6 +14,8 @@ CXXFLAGS ?= -O2 -std=c++17 -Wall -I include
 
 KERNEL_SRCS := $(CSRC)/kernels_build.hip $(CSRC)/kernels_bfs.hip $(CSRC)/kernels_parse.hip $(CSRC)/kernels_validate.hip
 HOST_SRCS   := $(CSRC)/bfsx_api.cpp $(CSRC)/bfsx_comm.cpp
+# every header a translation unit may include: an edit to any of them rebuilds the objects
+HDRS := $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h $(CSRC)/exchange_plan.h include/bfsx.h include/bfsx_levels.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 
 all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark tools/fetch_calib oracle
@@ -21,11 +23,11 @@ all: $(PKG)/libbfsx.so $(PKG)/bfsx_spark tools/fetch_calib oracle
 tools/fetch_calib: tools/fetch_calib.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
-$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h include/bfsx.h
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/%.o: $(CSRC)/%.cpp $(CSRC)/bfsx_internal.h $(CSRC)/java_digits.h include/bfsx.h
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

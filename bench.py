@@ -48,20 +48,19 @@ def load_module(name, file):
     return mod
 
 
-def level_bytes(ls, nwords, off_bytes=4):
+def level_bytes(ls, nwords, off_bytes=4, found_bytes=4):
     """Algorithmic bytes of one level: what the level must move at minimum, counted from
     its device counters.  Frontier-bit and visited-bit probes are not counted (the n/8-byte bitmaps are
     cache-resident).  off_bytes: width of the row offsets the traversal kernels read (uint32 when the
-    graph has < 2^32 adjacency entries)."""
+    graph has < 2^32 adjacency entries).  found_bytes: the store of a pull level's discovery (4: the
+    single-device 4-B parent, whose distance is the level record; 8: the partitioned loop's packed state)."""
     d = ls["direction"]
-    if d == 5:  # the pass that reached only deferred degree-1 vertices (leaf_defer): no kernels of its own
-        return 0
     if d in (2, 4):  # bottom-up (4: the sparse pull kernel of the tail levels, same accounting): visited word read + next word write, top1 of every live candidate, rest[]
         # (2nd..4th neighbours + degree, 16 B) of every top1 miss, the offset pair of each row walked past
-        # its first four entries (`claims`), the adjacency entries walked there, the packed state word
+        # its first four entries (`claims`), the adjacency entries walked there, the parent (or packed state)
         # of every vertex found
         return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 16 * ls["stage2"] + 2 * off_bytes * ls["claims"]
-                + 4 * ls["walked"] + 8 * ls["frontier_out"])
+                + 4 * ls["walked"] + found_bytes * ls["frontier_out"])
     if d == 3:  # hybrid: the pull half's bitmap pass + top1 of the live candidates, the push half's rows,
         # the state word of every vertex found
         return 16 * nwords + 4 * max(ls["unvisited_in"], 0) + 4 * max(ls["scanned"], 0) + 8 * ls["frontier_out"]
@@ -186,15 +185,15 @@ class LevelAccount:
     """Algorithmic bytes of the timed BFS runs: per bottom-up launch (the dominant kernel) and summed
     over every level of every BFS (the whole-BFS figure)."""
 
-    def __init__(self, nwords, off_bytes):
-        self.nwords, self.off_bytes = nwords, off_bytes
+    def __init__(self, nwords, off_bytes, found_bytes=4):
+        self.nwords, self.off_bytes, self.found_bytes = nwords, off_bytes, found_bytes
         self.bu_bytes, self.bu_ms, self.bu_launches = 0, 0.0, 0
         self.all_bytes = 0
         self.by_dir = {1: 0, 2: 0, 3: 0}
 
     def add(self, levels):
         for ls in levels:
-            b = level_bytes(ls, self.nwords, self.off_bytes)
+            b = level_bytes(ls, self.nwords, self.off_bytes, self.found_bytes)
             self.all_bytes += b
             self.by_dir[ls["direction"]] = self.by_dir.get(ls["direction"], 0) + b
             if ls["direction"] == 2:
@@ -381,6 +380,7 @@ def run_single(args):
             g.bfs_device_only(r)
 
     acct = LevelAccount(nwords, off_bytes)
+    pf0 = g.persist_fallbacks()
     ctx.synchronize()
     w0 = time.perf_counter()
     t_bfs, order, raw = [], [], []
@@ -391,18 +391,29 @@ def run_single(args):
             raw.append(g.level_stats_raw(256))  # decoded after the timed region
     ctx.synchronize()
     wall = time.perf_counter() - w0
+    persist_fallbacks = g.persist_fallbacks() - pf0
     all_levels = account_levels(acct, g, order, raw, args.levels_json)
 
     gteps = [mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(order, t_bfs)]
-    # output conversion (outside t_bfs): the unpack kernel that turns the packed internal-id state into the
-    # original-id int32 dist / parent arrays the C-ABI promises, then the PCIe copy of dist + int64 parent
-    unpack_ms, d2h_ms = [], []
+    # output conversion (outside t_bfs): the unpack kernel that turns the internal-id state (+ the pull levels'
+    # records) into one (parent, dist) word per original id, device only, for every root: GTEPS with the
+    # promised output materialised on the device (value_with_output)
+    unpack_ms, with_out = [], []
+    for r in roots:
+        t = g.bfs_device_only(r)
+        u = g.unpack_device_only()
+        unpack_ms.append(u)
+        with_out.append(mcomp[r] / ((t + u) * 1e-3) / 1e9)
+    # then the whole bfsx_result call into caller-owned host arrays (allocated and touched once, as a caller
+    # reusing its buffers would): unpack + D2H through pinned chunks + the split into int32 dist / int64 parent
+    d2h_ms = []
+    hd, hp = np.zeros(nv, np.int32), np.zeros(nv, np.int64)
     for r in roots[:4]:
         g.bfs_device_only(r)
         c0 = time.perf_counter()
-        g.result(want_parent=True)
+        g.result(want_parent=True, dist=hd, parent=hp)
         d2h_ms.append((time.perf_counter() - c0) * 1e3)
-        unpack_ms.append(g.last_unpack_ms())
+    del hd, hp
     cpu = serial = None
     if not args.no_cpu_baseline and args.cpu_baseline_seconds > 0 and g.nnz < (1 << 32):
         cpu, serial = cpu_baselines(args, g, roots, mcomp, nv)
@@ -416,10 +427,15 @@ def run_single(args):
     out["edge_scan_equivalent"] = edge_scan_equivalent(g.m, nv, float(np.mean(t_bfs)))
     out.update({"t_bfs_ms_mean": float(np.mean(t_bfs)), "t_bfs_ms_min": float(np.min(t_bfs)),
                 "t_unpack_ms": round(float(np.mean(unpack_ms)), 4),
+                "value_with_output": hmean(with_out),
                 "t_result_copy_ms": round(float(np.mean(d2h_ms)), 3),
-                "output_note": "t_unpack_ms: device time of the unpack kernel (internal-id packed state -> "
-                               "original-id int32 dist + parent), outside t_bfs; t_result_copy_ms: host wall "
-                               "time of bfsx_result (unpack + D2H of dist and int64 parent), 4 roots",
+                "output_note": "t_unpack_ms: device time of the unpack kernel (internal-id state + the pull levels' "
+                               "records -> one (parent, dist) word per original id), outside t_bfs, mean over the "
+                               "roots; value_with_output: harmonic-mean GTEPS over t_bfs + t_unpack (the promised "
+                               "output materialised on the device); t_result_copy_ms: host wall time of bfsx_result "
+                               "into reused caller arrays (unpack + D2H through pinned chunks + split into int32 dist "
+                               "and int64 parent), 4 roots",
+                "persist_fallbacks": persist_fallbacks,
                 "bfs_runs": len(t_bfs), "m_comp_mean": float(np.mean([mcomp[r] for r in order])),
                 "graph_build_s": round(build_s, 3),
                 "validation": {"roots": len(roots), "errors": val_errors, "skipped_tiny_component": skipped,
@@ -486,7 +502,7 @@ def run_dist(args, world, rank, local_rank):
             g.dist_bfs(r, want_stats=False)
 
     off_bytes = 4 if g.nnz < 0xFFFFFFFF and "offset_bits=64" not in args.option else 8
-    acct = LevelAccount(part["chunk"] // 64, off_bytes)
+    acct = LevelAccount(part["chunk"] // 64, off_bytes, found_bytes=8)
     # The K steps run back to back between two barrier + device-synchronise brackets (the contract's
     # timed region); every BFS is collective, so the ranks stay in step through its RCCL calls.
     ctx.synchronize()

@@ -36,7 +36,7 @@ EXPORTS = [
     "bfsx_result", "bfsx_level_times", "bfsx_level_dirs", "bfsx_level_stats",
     "bfsx_device_synchronize", "bfsx_validate", "bfsx_validate_result",
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
-    "bfsx_last_bfs_ms", "bfsx_last_unpack_ms", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group",
+    "bfsx_last_bfs_ms", "bfsx_last_unpack_ms", "bfsx_persist_fallbacks", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group",
     "bfsx_dist_bfs",
 ]
 # test-only level primitives (include/bfsx_levels.h): exported for tests/dist_driver.py, not product ABI
@@ -112,6 +112,7 @@ def lib():
         L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_last_bfs_ms.argtypes = [_VP, C.POINTER(C.c_double)]
         L.bfsx_last_unpack_ms.argtypes = [_VP, C.POINTER(C.c_double)]
+        L.bfsx_persist_fallbacks.argtypes = [_VP, C.POINTER(C.c_int64)]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
         L.bfsx_device_synchronize.argtypes = [_VP]
         I64P = C.POINTER(C.c_int64)
@@ -319,9 +320,27 @@ class Graph:
         _check(lib().bfsx_last_unpack_ms(self._h, C.byref(ms)))
         return ms.value
 
-    def result(self, want_parent=True):
-        dist = np.empty(self.nv, np.int32)
-        parent = np.empty(self.nv, np.int64) if want_parent else None
+    def persist_fallbacks(self):
+        """BFS runs of this graph re-run without K3p since it was built (bfsx_persist_fallbacks)."""
+        n = C.c_int64()
+        _check(lib().bfsx_persist_fallbacks(self._h, C.byref(n)))
+        return n.value
+
+    def unpack_device_only(self):
+        """Materialise the most recent result on the device only (bfsx_result with null outputs); returns the
+        unpack kernel's device time (ms)."""
+        _check(lib().bfsx_result(self._h, None, None))
+        return self.last_unpack_ms()
+
+    def result(self, want_parent=True, dist=None, parent=None):
+        """Copy the most recent result to host (bfsx_result); dist / parent: caller arrays to fill (reused
+        buffers), else new ones."""
+        if dist is None:
+            dist = np.empty(self.nv, np.int32)
+        if parent is None and want_parent:
+            parent = np.empty(self.nv, np.int64)
+        assert dist.dtype == np.int32 and dist.size == self.nv and dist.flags.c_contiguous
+        assert parent is None or (parent.dtype == np.int64 and parent.size == self.nv and parent.flags.c_contiguous)
         _check(lib().bfsx_result(self._h, _p(dist), _p(parent)))
         return dist, parent
 

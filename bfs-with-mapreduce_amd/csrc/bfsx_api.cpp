@@ -351,12 +351,6 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.test_overread = (int)x;
         return BFSX_OK;
     }
-    if (k == "leaf_defer") {
-        if (v == "on") ctx->opt.leaf_defer = true;
-        else if (v == "off") ctx->opt.leaf_defer = false;
-        else return fail(BFSX_E_ARG, "leaf_defer must be on|off");
-        return BFSX_OK;
-    }
     if (k == "leaf_skip") {
         if (v == "on") ctx->opt.leaf_skip = true;
         else if (v == "off") ctx->opt.leaf_skip = false;
@@ -898,6 +892,12 @@ int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms) {
     if (!g || !ms) return fail(BFSX_E_ARG, "bad argument");
     if (g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
     *ms = g->last_t_bfs_ms;
+    return BFSX_OK;
+}
+
+int bfsx_persist_fallbacks(const bfsx_graph *g, int64_t *count) {
+    if (!g || !count) return fail(BFSX_E_ARG, "bad argument");
+    *count = bfs_persist_fallbacks(g);
     return BFSX_OK;
 }
 

@@ -32,8 +32,8 @@ struct Options {
     int direction = BFSX_DIR_AUTO;
     int alpha = 20;             // top-down -> bottom-up when m_f > m_u / alpha (re-tuned on scale 26 with the
                                 // two-stage bottom-up: 20 vs 30 = +2%, within run-to-run noise of 10..45)
-    int beta = 24;
-    int64_t pull_min_edges = (int64_t)1 << 16; // push -> pull needs at least this many frontier edges (and n/512)              // bottom-up -> top-down when n_f < n / beta (and shrinking)
+    int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
+    int64_t pull_min_edges = (int64_t)1 << 16; // push -> pull needs at least this many frontier edges (and n/512)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
     int persist_blocks = 0;     // K3p workgroups (0: one per CU)
@@ -50,9 +50,6 @@ struct Options {
     // on every rank (read at a graph's first partitioned BFS; see dist_big_list)
     int64_t big_degree = 4096;
     bool leaf_skip = true;      // single device: a pull level's degree-1 discoveries stay out of the next push queue
-    // single device: the degree-1 tail of the id space (ids >= leaf_lo) stays out of the level loop -- pre-visited,
-    // never claimed by a push -- and is resolved from its one neighbour after the last level (k_finalize)
-    bool leaf_defer = false;
     int64_t big_cap = (int64_t)1 << 20;
     int hybrid = 1;             // hybrid levels (hub pull + non-hub push): 0 off, 1 auto (cost model), 2 force
     int hybrid_pct = 125;       // auto: hybrid when the frontier's hub edges exceed this % of the unvisited count
@@ -113,7 +110,7 @@ int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
 int64_t bfs_persist_fallbacks(const bfsx_graph *g); // BFS runs re-run without K3p after a barrier abort
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
-// device time (ms) of the most recent copy's unpack kernel (packed state -> original-id dist/parent); -1: none
+// device time (ms) of the most recent copy's unpack kernel (state + level records -> original-id dist/parent); -1: none
 double bfs_last_unpack_ms(const bfsx_graph *g);
 // multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
@@ -127,8 +124,11 @@ int dist_finish(bfsx_graph *g);
 // the whole partitioned level loop with the exchanges through ctx->comm (collective over the ranks)
 int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 void bfs_workspace_free(BfsWorkspace *ws);
-// packed state (parent << 32 | dist) of the most recent BFS (device; null before the first one)
+// packed state (parent << 32 | dist) of the most recent BFS (device; null before the first one).  Valid after
+// bfs_resolve: a single-device BFS leaves its pull levels' discoveries in their level records (4-B parents +
+// one bitmap per pull level) until then.
 const unsigned long long *bfs_state(const bfsx_graph *g);
+int bfs_resolve(bfsx_graph *g);
 // ---- kernels_validate.hip: Graph500-style validation of the most recent result --------------------
 // res = {violating vertices, smallest violating id (-1: none), reached, adjacency entries checked};
 // collective on a partitioned graph.  stt: packed states of the local rows to check (device), null =

@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstring>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -91,6 +93,15 @@ struct alignas(64) Published {
 struct BfsWorkspace {
     int64_t nv = 0, nwords = 0;
     u64 *st = nullptr;                  // packed parent << 32 | dist
+    // Pull levels (single device) store only a 4-B parent, par[v]; their discoveries are the level's record
+    // bitmap prec[k] (the `next` bitmap k_bu writes anyway, kept per level instead of swapped), which gives
+    // them distance prec_lvl[k] + 1.  st[v] of such a vertex is stale until bfs_resolve (or the fused unpack)
+    // reads the records -- outside the timed region, like the unpack to original ids.
+    uint32_t *par = nullptr;
+    std::vector<u64 *> prec;            // record pool (grown on demand, kept across BFS runs)
+    std::vector<int32_t> prec_nd;       // distance of record k's vertices (its level + 1), last BFS
+    int n_prec = 0;                     // records of the last BFS
+    bool resolved = true;               // st holds every reached vertex's state (no record pending)
     uint32_t *off32 = nullptr;          // uint32 copy of the row offsets (nnz < 2^32), else null
     u64 *vis = nullptr, *front = nullptr, *next = nullptr;
     u64 *dead = nullptr;                // isolated vertices + padding (initial visited bitmap)
@@ -110,13 +121,6 @@ struct BfsWorkspace {
     // discovered leaf's only neighbour is its parent, so a push level after a pull level leaves the
     // leaves of its bitmap frontier out of its queue (option leaf_skip)
     int64_t leaf_lo = 0;
-    // option leaf_defer (single device): the visited-bitmap start with every id >= leaf_lo set (`dead` plus the
-    // degree-1 tail), their number, this BFS's push-claim limit (0: off) and a
-    // flag (device word: a deferred vertex lies one level beyond the core's deepest, set by k_finalize)
-    u64 *dlf = nullptr;
-    int64_t n_def = 0, leaf_hi = 0;
-    uint32_t defer_lo = 0;
-    u64 *d_leafmax = nullptr;
     // every id >= hub_row_lim has at most hub_deg adjacency entries (the id of the last row with more, + 1;
     // on a relabelled graph a short prefix): a pull level that found no vertex below it hands the next
     // push level a frontier without hubs (no hub bin, K3p-eligible).  Recomputed when hub_degree changes.
@@ -125,10 +129,13 @@ struct BfsWorkspace {
     uint32_t *colh = nullptr;           // [nnz] col with hub entries encoded kHubBit | h
     u64 *hfront = nullptr;              // [ceil(hub_k/64)] frontier bits of the hubs
     uint32_t *qa = nullptr, *qb = nullptr, *hubs = nullptr;
-    // result staging of bfsx_bfs / bfsx_result (int32 dist, int32 parent in original ids): its own
-    // buffers, allocated at the first copy -- never the frontier queues, whose stale words must not be
-    // result data and whose result data must not be frontier ids
-    int32_t *out_dist = nullptr, *out_par = nullptr;
+    // result staging of bfsx_bfs / bfsx_result (one word per original id: parent << 32 | dist, or int32 dist
+    // only): its own buffer, allocated at the first copy -- never the frontier queues, whose stale words must
+    // not be result data and whose result data must not be frontier ids -- and two pinned host chunks the D2H
+    // copy streams through while host threads split them into the caller's arrays
+    u64 *out64 = nullptr;
+    u64 *h_stage = nullptr;
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_unpack0 = nullptr, ev_unpack1 = nullptr;
     double last_unpack_ms = -1.0;       // device time of the most recent unpack (state -> original-id arrays)
     // mapped pinned word: 0, or 1 << 32 | id of the first out-of-range id a queue consumer met (id_ok)
@@ -428,7 +435,6 @@ struct Part {
     u64 *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
     u64 *remote_tail; // their allocation cursor
     u64 *err;         // mapped host word: set when a queue holds an id >= nrows (null: unchecked)
-    uint32_t defer_lo; // option leaf_defer: ids >= defer_lo are never claimed by a push (0: none)
     uint32_t nranks;
     // small partitioned push levels (fixed-slot exchange): remote pairs go straight into the send buffer's
     // per-destination slots [count, slot_cap pairs] (slot_cap 0: into `remote` for the counted exchange);
@@ -438,7 +444,6 @@ struct Part {
     u64 *slot_cursor;
     u64 *slot_arrive;
 };
-__device__ inline bool deferred(uint32_t v, uint32_t defer_lo) { return defer_lo && v >= defer_lo; }
 
 // Queue-entry guard.  Every kernel that reads vertex ids out of a frontier queue, the hub list or an
 // exchange buffer checks them against the rows it holds before using them as an index: a stale or
@@ -532,11 +537,13 @@ __device__ inline void slot_headers_if_last(const Part &pt) {
 
 // Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries; u = local row id)
 // in steps of kBS*kItems.  Block-uniform.  kDist: targets owned by another rank become remote pairs.
+// par != null (the push half of a hybrid level): a winner's parent also goes to the 4-B parent array, because the
+// level's discoveries are merged into the pull half's level record, whose vertices take their parent from there.
 template <bool kDist, class OffT, class ScanT, class Q>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                      int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
+                                      uint32_t *__restrict__ par, int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
                                       HubSet hs, u64 &acc_mfh, u64 &acc_nh) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
@@ -567,9 +574,10 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                 send = valid[k] && (v[k] / pt.chunk) != pt.rank;
                 vl = v[k] - pt.lo;
             }
-            if (valid[k] && !send && !deferred(vl, pt.defer_lo) && claim(vl, vis, attempts)) {
+            if (valid[k] && !send && claim(vl, vis, attempts)) {
                 win = true;
                 stt[vl] = pack_state(pu[k], nd);
+                if (par) par[vl] = pu[k];
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
                 acc_mf += dg;
                 acc_dmax = dg > acc_dmax ? dg : acc_dmax;
@@ -591,7 +599,7 @@ template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
-                                            LevelSlot *ring, int level, uint32_t hub_deg,
+                                            uint32_t *__restrict__ par, LevelSlot *ring, int level, uint32_t hub_deg,
                                             uint32_t *__restrict__ hubs, Part pt, int gsz, HubSet hs,
                                             HubSet skip, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
@@ -649,7 +657,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             scanned += total;
         }
         __syncthreads();
-        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt, rq,
+        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, par, nd, q, qout, &cn->qtail, pt, rq,
                               acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh);
         __syncthreads();
     }
@@ -664,7 +672,8 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
 template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
-                                                 u64 *vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
+                                                 u64 *vis, u64 *__restrict__ stt, uint32_t *__restrict__ par,
+                                                 LevelSlot *ring, int level,
                                                  Part pt, HubSet hs, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_scan[kHubBatch + 1];
@@ -722,7 +731,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
-        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, nd, q, qout, &cn->qtail, pt,
+        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, par, nd, q, qout, &cn->qtail, pt,
                               rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh);
         __syncthreads();
     }
@@ -790,7 +799,7 @@ template <class OffT, bool kHeavy>
 __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const uint32_t *t_scan, const int64_t *t_beg,
                                              const uint32_t *t_u, int n, const OffT *__restrict__ row_off,
                                              const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                             int32_t nd, HubSet hs, u64 heavy_deg, uint32_t defer_lo, u64 *sout,
+                                             int32_t nd, HubSet hs, u64 heavy_deg, u64 *sout,
                                              u64 *hout, uint32_t &s_n, uint32_t &s_hn, PersistCtl *ctl, u64 &acc_mf,
                                              u64 &attempts, u64 &acc_dmax, u64 &acc_mfh, u64 &acc_eh, u64 &acc_dmh) {
     const unsigned tid = threadIdx.x, lane = tid & 63u;
@@ -811,7 +820,6 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
             }
             v[k] = col[t_beg[lo] + (int64_t)(x - t_scan[lo])];
             pu[k] = t_u[lo];
-            valid[k] = !deferred(v[k], defer_lo); // option leaf_defer: resolved after the last level
         }
     }
     // the visited word and the target's row bounds in one round trip
@@ -882,8 +890,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
                                                     PersistOut *out, HubSet hs, int64_t bu_floor,
                                                     int inject_abort, u64 heavy_deg, uint32_t nrows, u64 *err,
-                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg,
-                                                    uint32_t defer_lo) {
+                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_hoff[kBS + 1];
@@ -1015,7 +1022,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             if (tid == 0) scanned += total;
             __syncthreads();
             for (uint32_t x0 = 0; x0 < total; x0 += kBS * kItems)
-                persist_step<OffT, kHeavy>(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout, hout, s_n,
+                persist_step<OffT, kHeavy>(x0, total, s_scan, s_beg, s_u, n, row_off, col, vis, stt, nd, hs, heavy_deg, sout, hout, s_n,
                              s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
             __syncthreads();
         }
@@ -1024,7 +1031,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             const uint32_t xb = (uint32_t)(eh_in * b / G), xe = (uint32_t)(eh_in * (b + 1) / G);
             if (tid == 0) scanned += xe - xb;
             for (uint32_t x0 = xb; x0 < xe; x0 += kBS * kItems)
-                persist_step<OffT, kHeavy>(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, defer_lo, sout,
+                persist_step<OffT, kHeavy>(x0, xe, s_hscan, s_hb, s_hv, (int)nh_in, row_off, col, vis, stt, nd, hs, heavy_deg, sout,
                              hout, s_n, s_hn, ctl, acc_mf, attempts, acc_dmax, acc_mfh, acc_eh, acc_dmh);
         }
         // test hook (option "persist_abort_at"): every workgroup takes the abort path at this level, as a
@@ -1119,6 +1126,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+            // a workgroup whose segment overflowed (its record's count exceeds kRegion; it also raised ctl->abort)
+            // makes every workgroup take the abort path at THIS level, before any s_off is built from that count
+            if (tid < G && (w[0] & k24) > (u64)kRegion) s_ok = 0;
             __syncthreads();
             if (!s_ok) {
                 if (b == 0 && tid == 0) {
@@ -1442,13 +1452,22 @@ constexpr uint32_t kPrefIds = 1u << 16; // LDS frontier prefix: 8 KiB per workgr
 struct PrefixSpec {
     uint32_t ids, nseg, shift, pad;
 };
+// A pull level's discovery: single device, the 4-B parent only (the level's record bitmap gives the distance,
+// BfsWorkspace::par); partitioned (par_out == null), the packed state.
+__device__ __forceinline__ void settle_state(u64 *__restrict__ stt, uint32_t *__restrict__ par_out, uint32_t v,
+                                             uint32_t parent, int32_t nd) {
+    if (par_out) par_out[v] = parent;
+    else stt[v] = pack_state(parent, nd);
+}
+
 // kSpill: a diagnostic instantiation compiled for 8 waves per SIMD (64 VGPRs), so it spills to scratch --
 // option bu_force_spill, the round-2 "spilling pull kernel + concurrent in-process ranks" experiment.
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe, bool kSpill = false>
 __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
-                                            u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level,
+                                            u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out,
+                                            LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
                                             const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo,
                                             PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim) {
@@ -1611,7 +1630,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         }
                     }
                     if (found) {
-                        stt[v[k]] = pack_state(probe_id<kHubs>(hub_id, par), nd);
+                        settle_state(stt, par_out, v[k], probe_id<kHubs>(hub_id, par), nd);
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
                         if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
@@ -1671,7 +1690,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         acc_wk += (uint32_t)(j - b - 4);
                         acc_rows += 1;
                         if (found) {
-                            stt[vv] = pack_state(probe_id<kHubs>(hub_id, par), nd);
+                            settle_state(stt, par_out, vv, probe_id<kHubs>(hub_id, par), nd);
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
                             if (kMf) acc_mf += (uint32_t)(e - b);
@@ -1705,11 +1724,13 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
 #define BFSX_K_BU_PARAMS                                                                                        \
     const OffT *__restrict__ row_off, const uint32_t *__restrict__ col, const uint32_t *__restrict__ top1,      \
         const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next,                  \
-        u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring, int level, int64_t nwords, uint32_t fmask, \
+        u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out, LevelSlot *ring, int level,   \
+        int64_t nwords, uint32_t fmask,                                                                        \
         const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo, \
         PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim
 #define BFSX_K_BU_ARGS                                                                                          \
-    row_off, col, top1, rest, front, next, vis, stt, ring, level, nwords, fmask, hfront, hub_id, hub_lim, leaf_lo, pf, \
+    row_off, col, top1, rest, front, next, vis, stt, par_out, ring, level, nwords, fmask, hfront, hub_id, hub_lim,     \
+        leaf_lo, pf,                                                                                           \
         pub, seq, hub_row_lim
 
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe>
@@ -1742,7 +1763,8 @@ template <class OffT>
 __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                    const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                                    const u64 *__restrict__ front, u64 *__restrict__ next,
-                                                   u64 *__restrict__ vis, u64 *__restrict__ stt, LevelSlot *ring,
+                                                   u64 *__restrict__ vis, u64 *__restrict__ stt,
+                                                   uint32_t *__restrict__ par_out, LevelSlot *ring,
                                                    int level, int64_t nwords, uint32_t fmask, uint32_t hub_row_lim,
                                                    uint32_t qlim, uint32_t *__restrict__ qout, Published *pub,
                                                    u64 seq) {
@@ -1761,7 +1783,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
     // state word + next-frontier bit of a found vertex; wave-uniform queue append of the ones below qlim
     auto settle = [&](bool found, uint32_t v, uint32_t par) {
         if (found) {
-            stt[v] = pack_state(par, nd);
+            settle_state(stt, par_out, v, par, nd);
             atomicOr(&s_nx[wave][(int64_t)(v >> 6) - wb], 1ull << (v & 63u));
             acc_nf += 1;
             acc_nh += v < hub_row_lim ? 1u : 0u;
@@ -2018,94 +2040,14 @@ __global__ __launch_bounds__(kBS) void k_bitmap_to_queue(const u64 *__restrict__
 // After the last level: vertices left unvisited in this BFS (and not isolated) become WHITE again
 // (INT32_MAX, no parent), so the per-BFS init never rewrites the whole state array (isolated vertices
 // keep the value written once when the workspace is created).
-//
-// Option leaf_defer: the same launch resolves the deferred degree-1 tail [leaf_lo, nv) (pre-visited, never
-// claimed): a non-isolated v there has exactly one neighbour u = top1[v]; v is reached iff u is -- u is the
-// source, or a core vertex (u < leaf_lo) whose visited bit is set -- and then takes parent u and u's distance
-// + 1, else it is WHITE.  The two loops touch disjoint states (unreached core vertices vs deferred ones, whose
-// parents are reached core vertices).  One coalesced top1 load and state store per deferred vertex; the
-// parents' states and visited words are the dense low-id lines.  *deep = 1 when one of them lies at
-// distance deep_d (one beyond the core's deepest: the whole BFS has one more pass).
-// Blocks [0, wblocks) sweep the visited words (grid-stride); every further block resolves kBS consecutive
-// deferred ids [leaf_lo, leaf_hi), one per thread, so the deferred range is covered in one wave of loads
-// (a grid-stride loop over it ran ~80 dependent iterations per thread: 250 us at scale 26).
-constexpr int kLeafItems = 8;
-__global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ stt,
-                                                  unsigned wblocks, const uint32_t *__restrict__ top1, uint32_t flag,
-                                                  int64_t leaf_lo, int64_t leaf_hi, uint32_t src, uint32_t deep_d,
-                                                  u64 *deep) {
-    if (blockIdx.x < wblocks) {
-        for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)wblocks * kBS) {
-            u64 u = ~vis[w];
-            while (u) {
-                const int b = __ffsll((long long)u) - 1;
-                stt[w * 64 + b] = kUnreached;
-                u &= u - 1ull;
-            }
-        }
-        return;
-    }
-    // kLeafItems deferred ids per thread, strided by kBS (coalesced top1 loads and state stores), every
-    // dependent load issued for all of them before the next: top1 -> {neighbour's visited word, neighbour's
-    // state}.  A self-loop-only row's top1 is itself (>= leaf_lo): WHITE, no loads.  The neighbours' states
-    // are gathered from all over the state array (one line per deferred vertex): that gather is what the
-    // pass costs.
-    const int64_t i0 = leaf_lo + (int64_t)(blockIdx.x - wblocks) * kBS * kLeafItems + threadIdx.x;
-    uint32_t p[kLeafItems], v[kLeafItems];
-#pragma unroll
-    for (int k = 0; k < kLeafItems; k++) {
-        const int64_t x = i0 + (int64_t)k * kBS;
-        v[k] = x < leaf_hi ? (uint32_t)x : 0xFFFFFFFFu;
-        p[k] = x < leaf_hi ? top1[x] & ~flag : 0xFFFFFFFFu;
-    }
-    u64 vw[kLeafItems], sp[kLeafItems];
-#pragma unroll
-    for (int k = 0; k < kLeafItems; k++) {
-        const bool core = (int64_t)p[k] < leaf_lo;
-        vw[k] = core ? vis[p[k] >> 6] : 0ull;
-        sp[k] = core ? stt[p[k]] : 0ull;
-    }
-    bool is_deep = false;
-#pragma unroll
-    for (int k = 0; k < kLeafItems; k++) {
-        if (v[k] == 0xFFFFFFFFu || v[k] == src) continue;
-        const bool core = (int64_t)p[k] < leaf_lo;
-        u64 s = kUnreached;
-        if (p[k] == src) {
-            s = pack_state(p[k], 1);
-            is_deep |= deep_d == 1u;
-        } else if (core && ((vw[k] >> (p[k] & 63u)) & 1ull)) {
-            const uint32_t d = (uint32_t)sp[k] + 1u;
-            s = pack_state(p[k], (int32_t)d);
-            is_deep |= d == deep_d;
-        }
-        stt[v[k]] = s;
-    }
-    // a deferred vertex one level beyond the core's deepest: the whole BFS has one more pass.  One plain store
-    // of the same value per wave that holds one (an atomic max per wave serialised 134 K same-address atomics:
-    // 1.5 ms at scale 26)
-    const u64 dm = __ballot(is_deep);
-    if (dm && (int)lane_id() == __ffsll((long long)dm) - 1) *deep = 1ull;
-}
-
-// 1 + the largest id whose row holds an entry other than itself (the end of the deferred range)
-__global__ __launch_bounds__(kBS) void k_last_live(const u64 *__restrict__ dead, int64_t nwords, u64 *out) {
-    u64 best = 0;
+__global__ __launch_bounds__(kBS) void k_finalize(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ stt) {
     for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
-        const u64 m = ~dead[w];
-        if (m) best = max(best, (u64)(w * 64 + 64 - __clzll((long long)m)));
-    }
-    best = wave_max(best);
-    if (lane_id() == 0 && best) atomicMax(out, best);
-}
-
-// leaf_defer: the BFS's starting visited bitmap = dead | every id >= leaf_lo
-__global__ __launch_bounds__(kBS) void k_leaf_mask(const u64 *__restrict__ dead, int64_t nwords, int64_t leaf_lo,
-                                                   u64 *__restrict__ out) {
-    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
-        const int64_t b = w * 64;
-        const u64 m = b >= leaf_lo ? ~0ull : (b + 64 <= leaf_lo ? 0ull : ~0ull << (leaf_lo - b));
-        out[w] = dead[w] | m;
+        u64 u = ~vis[w];
+        while (u) {
+            const int b = __ffsll((long long)u) - 1;
+            stt[w * 64 + b] = kUnreached;
+            u &= u - 1ull;
+        }
     }
 }
 
@@ -2113,26 +2055,62 @@ __global__ __launch_bounds__(kBS) void k_fill64(u64 *__restrict__ p, int64_t n, 
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) p[i] = val;
 }
 
-// Result extraction (outside the timed region): packed state -> int32 dist + int32 parent.
-__global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, int64_t n, int32_t *__restrict__ dist,
-                                                int32_t *__restrict__ parent) {
-    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
-        const u64 s = stt[i];
-        dist[i] = (int32_t)(uint32_t)s;
-        parent[i] = (int32_t)(uint32_t)(s >> 32);
+// ---- pull-level records (single device, BfsWorkspace::par) ----------------------------------------
+// At most kMaxRec records per BFS; a BFS with more pull levels folds its records into st mid-BFS (k_resolve).
+constexpr int kMaxRec = 32;
+struct RecSet {
+    const u64 *bm[kMaxRec];
+    int32_t nd[kMaxRec]; // distance of the record's vertices (its level + 1)
+    int n;
+};
+
+// state of internal vertex i: st[i], unless a record holds i (its parent is then par[i]).  Lanes of consecutive
+// i share their record words (one broadcast load per wave and record).
+__device__ __forceinline__ u64 rec_state(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
+                                         const RecSet &rs, int64_t i) {
+    for (int r = 0; r < rs.n; r++)
+        if ((rs.bm[r][i >> 6] >> (i & 63)) & 1ull) return pack_state(par[i], rs.nd[r]);
+    return stt[i];
+}
+
+// st[v] = (par[v], nd_r) for every vertex v of every record r (the validator's and m_comp's view of a result;
+// a BFS with more than kMaxRec pull levels).  One wave per bitmap word, lane = bit: a word's par loads and state
+// stores are one coalesced access each.
+__global__ __launch_bounds__(kBS) void k_resolve(RecSet rs, int64_t nwords, const uint32_t *__restrict__ par,
+                                                 u64 *__restrict__ stt) {
+    const unsigned lane = lane_id();
+    const int64_t nwaves = ((int64_t)gridDim.x * kBS) >> 6;
+    for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords; w += nwaves) {
+        for (int r = 0; r < rs.n; r++) {
+            const u64 m = rs.bm[r][w];
+            if (m == 0ull) continue; // wave-uniform
+            if ((m >> lane) & 1ull) {
+                const int64_t v = w * 64 + lane;
+                stt[v] = pack_state(par[v], rs.nd[r]);
+            }
+        }
     }
 }
 
-// The same for a relabelled graph: internal local row i is original vertex inv[lo + i] (a partition's
-// relabel keeps it inside the rank's range [lo, lo + n)); parents are global internal ids and map back too.
-__global__ __launch_bounds__(kBS) void k_unpack_relabel(const u64 *__restrict__ stt, const uint32_t *__restrict__ inv,
-                                                        int64_t lo, int64_t n, int32_t *__restrict__ dist,
-                                                        int32_t *__restrict__ parent) {
+// Result extraction (outside the timed region): internal state (+ the pending records) -> one 8-byte word per
+// ORIGINAL id, out[o] = parent_original << 32 | dist (one scattered store per vertex where separate dist and
+// parent arrays took two), or dist only.  kRelabel: internal local row i is original vertex inv[lo + i] (a
+// partition's relabel keeps it inside the rank's range [lo, lo + n)); parents are global internal ids and map
+// back through the whole inv.
+template <bool kRelabel>
+__global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
+                                                RecSet rs, const uint32_t *__restrict__ inv, int64_t lo, int64_t n,
+                                                u64 *__restrict__ out, int32_t *__restrict__ dist_only) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
-        const u64 s = stt[i];
-        const uint32_t o = (uint32_t)((int64_t)inv[lo + i] - lo), p = (uint32_t)(s >> 32);
-        dist[o] = (int32_t)(uint32_t)s;
-        parent[o] = p == 0xFFFFFFFFu ? -1 : (int32_t)inv[p];
+        const u64 s = rec_state(stt, par, rs, i);
+        const uint32_t o = kRelabel ? (uint32_t)((int64_t)inv[lo + i] - lo) : (uint32_t)i;
+        if (dist_only) {
+            dist_only[o] = (int32_t)(uint32_t)s;
+        } else {
+            const uint32_t p = (uint32_t)(s >> 32);
+            const uint32_t po = (!kRelabel || p == 0xFFFFFFFFu) ? p : inv[p];
+            out[o] = ((u64)po << 32) | (uint32_t)s;
+        }
     }
 }
 
@@ -2453,6 +2431,7 @@ int ws_alloc(bfsx_graph *g) {
     ws->nwords = g->chunk / 64;
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
     BFSX_HIP_TRY(hipMalloc(&ws->st, nv * sizeof(u64)));
+    if (g->nranks == 1) BFSX_HIP_TRY(hipMalloc(&ws->par, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(u64)));
@@ -2504,26 +2483,6 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     ws->n_dead = (int64_t)nd[0] - (ws->nwords * 64 - g->nv); // minus padding bits
     ws->leaf_lo = (int64_t)nd[1];
-    if (g->nranks == 1 && ws->leaf_lo < g->nv) { // option leaf_defer: the start bitmap with the degree-1 tail set
-        BFSX_HIP_TRY(hipMalloc(&ws->dlf, ws->nwords * sizeof(u64)));
-        BFSX_HIP_TRY(hipMalloc(&ws->d_leafmax, sizeof(u64)));
-        hipLaunchKernelGGL(k_leaf_mask, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
-                           ws->dead, ws->nwords, ws->leaf_lo, ws->dlf);
-        BFSX_LAUNCHED(st);
-        BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, sizeof(u64), st));
-        hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dlf,
-                           ws->nwords, ws->d_red);
-        BFSX_LAUNCHED(st);
-        BFSX_HIP_TRY(hipMemsetAsync(ws->d_red + 1, 0, sizeof(u64), st));
-        hipLaunchKernelGGL(k_last_live, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st,
-                           ws->dead, ws->nwords, ws->d_red + 1);
-        BFSX_LAUNCHED(st);
-        u64 nl[2] = {0, 0};
-        BFSX_HIP_TRY(hipMemcpyAsync(nl, ws->d_red, sizeof(nl), hipMemcpyDeviceToHost, st));
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
-        ws->n_def = (int64_t)nl[0] - (int64_t)nd[0]; // the deferred (non-isolated) vertices
-        ws->leaf_hi = std::max<int64_t>(std::min<int64_t>((int64_t)nl[1], g->nv), ws->leaf_lo);
-    }
     return BFSX_OK;
 }
 
@@ -2532,7 +2491,6 @@ Part single_part(const bfsx_graph *g, const BfsWorkspace *ws) {
     Part p{};
     p.nrows = (uint32_t)g->nv;
     p.err = ws->d_err;
-    p.defer_lo = ws->defer_lo;
     return p;
 }
 
@@ -2593,7 +2551,7 @@ bool has_hubs(const BfsWorkspace *ws) { return ws->hub_k > 0 || ws->hub_lim > 0;
 // pub != null: the last kernel launched publishes the level's counters (seq) from its last workgroup
 template <bool kDist>
 int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt,
-              bool skip_hubs = false, Published *pub = nullptr, u64 seq = 0) {
+              bool skip_hubs = false, Published *pub = nullptr, u64 seq = 0, uint32_t *par = nullptr) {
     hipStream_t st = g->ctx->stream;
     const HubSet hs = hub_set(ws);
     const HubSet skip = skip_hubs ? hs : HubSet{0xFFFFFFFFu, 0u};
@@ -2610,22 +2568,22 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     if (hubs) pt0.slot_arrive = nullptr;
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
+                           ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
                            hubs ? nullptr : pub, seq);
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs, pub, seq);
+                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq);
             BFSX_LAUNCHED(st);
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
                            hubs ? nullptr : pub, seq);
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, ws->ring, level, pt, hs, pub, seq);
+                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq);
             BFSX_LAUNCHED(st);
         }
     }
@@ -2650,8 +2608,8 @@ PrefixSpec lds_prefix(const bfsx_graph *g, const BfsWorkspace *ws) {
 }
 
 template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe, bool kSpill = false>
-int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
-                u64 seq) {
+int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, u64 *next, uint32_t *par,
+                int level, Published *pub, u64 seq) {
     hipStream_t st = g->ctx->stream;
     // persistent grid: exactly the resident workgroups (a partial second wave of workgroups would
     // leave most CUs idle at the tail of the grid-stride loop)
@@ -2673,7 +2631,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
     }
 #define BFSX_K_BU_LAUNCH(kern)                                                                                   \
     hipLaunchKernelGGL(kern, grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, \
-                       ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id,  \
+                       next, ws->vis, ws->st, par, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id,  \
                        ws->hub_lim, (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws),  \
                        pub, seq, (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll))
     if constexpr (kSpill) BFSX_K_BU_LAUNCH((k_bu_spill<OffT>));
@@ -2684,50 +2642,57 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
 }
 
 template <class OffT, bool kMf, bool kHubs>
-int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, int level, Published *pub,
-                u64 seq) {
-    if (g->ctx->opt.bu_unroll == 2) return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, level, pub, seq);
+int launch_bu_t(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 *front, u64 *next, uint32_t *par,
+                int level, Published *pub, u64 seq) {
+    if (g->ctx->opt.bu_unroll == 2)
+        return launch_bu_u<OffT, kMf, kHubs, 2, false, false>(g, ws, row_off, front, next, par, level, pub, seq);
     if (kMf && !kHubs && g->ctx->opt.bu_force_spill) // diagnostic (see k_bu's kSpill)
-        return launch_bu_u<OffT, kMf, false, 4, false, true, true>(g, ws, row_off, front, level, pub, seq);
+        return launch_bu_u<OffT, kMf, false, 4, false, true, true>(g, ws, row_off, front, next, par, level, pub, seq);
     // kMf (partitioned) + kPipe needs more than the 96 VGPRs of 5 waves per SIMD: that instantiation runs
     // at 4 waves per SIMD (a spilling pull kernel is never an option)
     return g->ctx->opt.bu_pipeline
-               ? launch_bu_u<OffT, kMf, kHubs, 4, false, true>(g, ws, row_off, front, level, pub, seq)
-               : launch_bu_u<OffT, kMf, kHubs, 4, false, false>(g, ws, row_off, front, level, pub, seq);
+               ? launch_bu_u<OffT, kMf, kHubs, 4, false, true>(g, ws, row_off, front, next, par, level, pub, seq)
+               : launch_bu_u<OffT, kMf, kHubs, 4, false, false>(g, ws, row_off, front, next, par, level, pub, seq);
 }
 
 // The bottom-up half of a hybrid level: candidates probe only the hubs of the frontier (single device).
-int launch_bu_hubonly(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level) {
+int launch_bu_hubonly(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, u64 *next, uint32_t *par, int level) {
     if (ws->hub_k > 0)
-        return ws->off32 ? launch_bu_u<uint32_t, false, true, 4, true, false>(g, ws, ws->off32, front, level, nullptr, 0)
-                         : launch_bu_u<int64_t, false, true, 4, true, false>(g, ws, g->d_row_off, front, level, nullptr, 0);
-    return ws->off32 ? launch_bu_u<uint32_t, false, false, 4, true, false>(g, ws, ws->off32, front, level, nullptr, 0)
-                     : launch_bu_u<int64_t, false, false, 4, true, false>(g, ws, g->d_row_off, front, level, nullptr, 0);
+        return ws->off32
+                   ? launch_bu_u<uint32_t, false, true, 4, true, false>(g, ws, ws->off32, front, next, par, level, nullptr, 0)
+                   : launch_bu_u<int64_t, false, true, 4, true, false>(g, ws, g->d_row_off, front, next, par, level, nullptr, 0);
+    return ws->off32
+               ? launch_bu_u<uint32_t, false, false, 4, true, false>(g, ws, ws->off32, front, next, par, level, nullptr, 0)
+               : launch_bu_u<int64_t, false, false, 4, true, false>(g, ws, g->d_row_off, front, next, par, level, nullptr, 0);
 }
 
+// par == null: discoveries store the packed state (the partitioned loop); else the 4-B parent (single device,
+// `next` is then the level's record)
 template <bool kMf>
-int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, int level, Published *pub = nullptr, u64 seq = 0) {
+int launch_bu(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, u64 *next, uint32_t *par, int level,
+              Published *pub = nullptr, u64 seq = 0) {
     if (ws->hub_k > 0) // top1 is hub-encoded: every bottom-up launch of this graph uses the hub domain
-        return ws->off32 ? launch_bu_t<uint32_t, kMf, true>(g, ws, ws->off32, front, level, pub, seq)
-                         : launch_bu_t<int64_t, kMf, true>(g, ws, g->d_row_off, front, level, pub, seq);
-    return ws->off32 ? launch_bu_t<uint32_t, kMf, false>(g, ws, ws->off32, front, level, pub, seq)
-                     : launch_bu_t<int64_t, kMf, false>(g, ws, g->d_row_off, front, level, pub, seq);
+        return ws->off32 ? launch_bu_t<uint32_t, kMf, true>(g, ws, ws->off32, front, next, par, level, pub, seq)
+                         : launch_bu_t<int64_t, kMf, true>(g, ws, g->d_row_off, front, next, par, level, pub, seq);
+    return ws->off32 ? launch_bu_t<uint32_t, kMf, false>(g, ws, ws->off32, front, next, par, level, pub, seq)
+                     : launch_bu_t<int64_t, kMf, false>(g, ws, g->d_row_off, front, next, par, level, pub, seq);
 }
 
 // The sparse pull kernel (tail levels): one wave per kSparseWords words.  The discoveries below qlim land in
 // ws->qa (the next push level's queue; its length is the published qtail).
-int launch_bu_sparse(bfsx_graph *g, BfsWorkspace *ws, int level, uint32_t qlim, Published *pub, u64 seq) {
+int launch_bu_sparse(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, u64 *next, uint32_t *par, int level,
+                     uint32_t qlim, Published *pub, u64 seq) {
     hipStream_t st = g->ctx->stream;
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     const dim3 grid(clamp_grid((ws->nwords + kWaves * kSparseWords - 1) / (kWaves * kSparseWords), cap));
     const uint32_t hrl = (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll);
     if (ws->off32)
         hipLaunchKernelGGL(k_bu_sparse<uint32_t>, grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->top1, ws->rest,
-                           ws->front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
+                           front, next, ws->vis, ws->st, par, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
                            ws->qa, pub, seq);
     else
         hipLaunchKernelGGL(k_bu_sparse<int64_t>, grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->top1, ws->rest,
-                           ws->front, ws->next, ws->vis, ws->st, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
+                           front, next, ws->vis, ws->st, par, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
                            ws->qa, pub, seq);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
@@ -2925,13 +2890,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
     else
         hipLaunchKernelGGL(kp64, grid, dim3(kBS), lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, ws->defer_lo);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
@@ -2959,13 +2924,17 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
-                    (void *)ws->d_dist_ctr, (void *)ws->out_dist, (void *)ws->out_par, (void *)ws->dlf,
-                    (void *)ws->d_leafmax})
+                    (void *)ws->d_dist_ctr, (void *)ws->out64})
         if (p) (void)hipFree(p);
     for (void *p : ws->retired) (void)hipFree(p);
+    for (void *p : ws->prec) (void)hipFree(p);
+    if (ws->par) (void)hipFree(ws->par);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
     if (ws->ev_unpack0) (void)hipEventDestroy(ws->ev_unpack0);
     if (ws->ev_unpack1) (void)hipEventDestroy(ws->ev_unpack1);
+    for (auto e : ws->ev_stage)
+        if (e) (void)hipEventDestroy(e);
+    if (ws->h_stage) (void)hipHostFree(ws->h_stage);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->h_pub) (void)hipHostFree(ws->h_pub);
     if (ws->h_pout) (void)hipHostFree(ws->h_pout);
@@ -2979,19 +2948,20 @@ void bfs_workspace_free(BfsWorkspace *ws) {
 
 namespace {
 
-int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist);
+int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist, bool record_start);
 
 } // namespace
 
 // K3p's grid barrier needs all of its workgroups resident; the launch is sized by the occupancy API,
 // but another context on the same device can still hold CUs.  A barrier that times out aborts the
 // launch (every workgroup exits), and the BFS is re-run from its source without K3p -- the level
-// loop is deterministic, so the result is the same.
+// loop is deterministic, so the result is the same.  The re-run keeps the first attempt's start event, so
+// t_bfs covers the aborted attempt too.
 int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
-    int rc = bfs_run_impl(g, source, stats, true);
+    int rc = bfs_run_impl(g, source, stats, true, true);
     if (rc == kPersistAborted) {
         g->ws->persist_fallbacks++;
-        rc = bfs_run_impl(g, source, stats, false);
+        rc = bfs_run_impl(g, source, stats, false, false);
     }
     return rc == kPersistAborted ? fail(BFSX_E_HIP, "persistent top-down aborted twice") : rc;
 }
@@ -3000,7 +2970,7 @@ int64_t bfs_persist_fallbacks(const bfsx_graph *g) { return g->ws ? g->ws->persi
 
 namespace {
 
-int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist) {
+int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist, bool record_start) {
     if (source < 0 || source >= g->nv)
         return fail(BFSX_E_RANGE, "source vertex " + std::to_string(source) + " outside [0, " +
                                       std::to_string(g->nv) + ")");
@@ -3018,23 +2988,14 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t src_off[2];
     BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
 
-    // option leaf_defer: the degree-1 tail starts visited and is resolved by k_finalize
-    // (not with the encoded hub probe domain of a graph built without the relabel: its top1 holds encoded ids)
-    const bool defer = opt.leaf_defer && ws->dlf != nullptr && ws->hub_k == 0;
-    ws->defer_lo = defer ? (uint32_t)ws->leaf_lo : 0u;
-    const int64_t n_pre = ws->n_dead + (defer ? ws->n_def : 0); // pre-visited non-padding ids
-    // Beamer's n of the pull -> push rule: with the tail deferred, n_f counts core vertices only, so the rule
-    // compares it with the core vertices (the ids neither isolated nor deferred)
-    const int64_t nbeta = defer ? std::max<int64_t>(g->nv - n_pre, 1) : g->nv;
-    if (defer) BFSX_HIP_TRY(hipMemsetAsync(ws->d_leafmax, 0, sizeof(u64), st));
+    const int64_t n_pre = ws->n_dead; // pre-visited non-padding ids
     if (opt.poison_queues) // test hook: a consumer that reads past a queue's tail meets 0xFFFFFFFF (id_ok)
         for (uint32_t *q : {ws->qa, ws->qb, ws->hubs})
             BFSX_HIP_TRY(hipMemsetAsync(q, 0xFF, (size_t)std::max<int64_t>(nv, 1) * sizeof(uint32_t), st));
     // ---- timed region: source init -> last level ----
-    BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
+    if (record_start) BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
-                       (uint32_t)source, ws->prev_source, defer ? ws->dlf : ws->dead, nwords, ws->st, ws->vis, ws->qa,
-                       ws->ring);
+                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_LAUNCHED(st);
     ws->prev_source = source;
 
@@ -3057,6 +3018,38 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // the last (sparse) pull level already wrote the next push level's queue into ws->qa (nf_core ids)
     bool queue_ready = false;
     int td_levels = 0, bu_levels = 0;
+    // the bitmap frontier: ws->front after a push -> pull conversion, a pull level's record after a pull level
+    const u64 *bmf = ws->front;
+    // pull-level records of this BFS (BfsWorkspace::par): every pull level writes its discoveries into a fresh
+    // one; a BFS with more than kMaxRec pull levels folds them into st (k_resolve) and starts over
+    int n_prec = 0;
+    int32_t rec_nd[kMaxRec];
+    ws->n_prec = 0;
+    ws->resolved = true;
+    auto rec_set = [&]() {
+        RecSet rs{};
+        rs.n = n_prec;
+        for (int r = 0; r < n_prec; r++) {
+            rs.bm[r] = ws->prec[r];
+            rs.nd[r] = rec_nd[r];
+        }
+        return rs;
+    };
+    auto take_rec = [&](u64 **out) -> int {
+        if (n_prec == kMaxRec) {
+            hipLaunchKernelGGL(k_resolve, dim3(clamp_grid((nwords * 64 + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                               rec_set(), nwords, ws->par, ws->st);
+            BFSX_LAUNCHED(st);
+            n_prec = 0; // the frontier (the last record) is read, not written, by the next pull level
+        }
+        while ((int)ws->prec.size() <= n_prec) {
+            u64 *b = nullptr;
+            BFSX_HIP_TRY(hipMalloc(&b, nwords * sizeof(u64)));
+            ws->prec.push_back(b);
+        }
+        *out = ws->prec[n_prec];
+        return BFSX_OK;
+    };
     std::vector<LevelTiming> timing;
     g->level_dirs.clear();
     g->level_cum_ms.clear();
@@ -3066,7 +3059,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         if (opt.direction == BFSX_DIR_AUTO && level > 0) {
             if (dir == BFSX_DIR_TOPDOWN) {
                 if (mf > mu / std::max(opt.alpha, 1) && mf > bu_floor(g, ws)) dir = BFSX_DIR_BOTTOMUP;
-            } else if (nf < nbeta / std::max(opt.beta, 1) && nf < prev_nf) {
+            } else if (nf < nv / std::max(opt.beta, 1) && nf < prev_nf) {
                 dir = BFSX_DIR_TOPDOWN;
             }
         }
@@ -3088,6 +3081,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         // walk their whole hub prefix), the push level ~0.028 ms per million frontier edges (0.72 ms at
         // 17.6 M, 1.74 ms at 67.4 M) -- so hybrid only once the hubs' edges exceed 1.25 U.
         bool hybrid = false, sparse = false;
+        u64 *bu_rec = nullptr; // a pull level's record
         if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && has_hubs(ws) && opt.hybrid != 0 && mfh > 0) {
             const int64_t unv = nv - visited - n_pre;
             hybrid = opt.hybrid == 2 || 100 * mfh > (int64_t)opt.hybrid_pct * unv;
@@ -3097,11 +3091,14 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->qa,
                                (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
             BFSX_LAUNCHED(st);
-            if (int e = launch_bu_hubonly(g, ws, ws->front, level)) return e; // -> next, vis, st
+            u64 *rec = nullptr;
+            if (int e = take_rec(&rec)) return e;
+            if (int e = launch_bu_hubonly(g, ws, ws->front, rec, ws->par, level)) return e; // -> rec, vis, par
             const Part pt = single_part(g, ws);
-            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true)) return e; // -> qb
+            // -> qb; its winners also store their parent in par (they join the record below)
+            if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true, nullptr, 0, ws->par)) return e;
             LevelSlot *cn = ws->ring + (level + 1) % 3;
-            hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, cn, ws->next, ws->d_pub,
+            hipLaunchKernelGGL(k_queue_to_bitmap_dev, dim3(cap), dim3(kBS), 0, st, ws->qb, cn, rec, ws->d_pub,
                                ++ws->pub_seq, (uint32_t)g->nv, ws->d_err);
             BFSX_LAUNCHED(st);
             BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
@@ -3136,7 +3133,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             in_queue = false;
             snapped = false;
             bu_levels++;
-            std::swap(ws->front, ws->next);
+            rec_nd[n_prec++] = level + 1;
+            bmf = rec;
             if (nf == 0) break;
             continue;
         }
@@ -3150,6 +3148,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                                    ws->qa, (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
             }
             BFSX_LAUNCHED(st);
+            bmf = ws->front;
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue && queue_ready) {
             // the sparse pull level queued its discoveries (the non-leaves with leaf_skip) itself
@@ -3166,7 +3165,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             const int64_t per_block_min = (int64_t)kBS * kCompactWords;
             const unsigned gb = clamp_grid(std::max<int64_t>((cw + per_block_min - 1) / per_block_min, 1), 256);
             const int64_t wpb = ((cw + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
-            hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, cw, wpb, ws->qa,
+            hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, bmf, cw, wpb, ws->qa,
                                ws->d_cursor, lim);
             BFSX_LAUNCHED(st);
             if (skip) nf = nf_core;
@@ -3241,10 +3240,12 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         } else {
             // few unvisited candidates (the tail levels): the sparse kernel, which also queues its discoveries
             sparse = opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - n_pre) * opt.bu_sparse <= nwords * 64;
+            if (int e = take_rec(&bu_rec)) return e;
             if (sparse) {
                 const uint32_t qlim = (uint32_t)(opt.leaf_skip ? std::min<int64_t>(ws->leaf_lo, nv) : nv);
-                if (int e = launch_bu_sparse(g, ws, level, qlim, ws->d_pub, ++ws->pub_seq)) return e;
-            } else if (int e = launch_bu<false>(g, ws, ws->front, level, ws->d_pub, ++ws->pub_seq)) {
+                if (int e = launch_bu_sparse(g, ws, bmf, bu_rec, ws->par, level, qlim, ws->d_pub, ++ws->pub_seq))
+                    return e;
+            } else if (int e = launch_bu<false>(g, ws, bmf, bu_rec, ws->par, level, ws->d_pub, ++ws->pub_seq)) {
                 return e;
             }
             bu_levels++;
@@ -3293,35 +3294,26 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             mf = -1;   // not accumulated by the single-GPU bottom-up step
             dmax = -1;
             mfh = -1;
-            std::swap(ws->front, ws->next);
+            rec_nd[n_prec++] = level + 1;
+            bmf = bu_rec;
         }
         if (nf == 0) break;
     }
-    // unvisited (non-isolated) vertices -> WHITE, deferred degree-1 vertices resolved; inside the timed region
-    {
-        const unsigned wb = clamp_grid((nwords + kBS - 1) / kBS, cap);
-        const int64_t nleaf = defer ? ws->leaf_hi - ws->leaf_lo : 0;
-        const int64_t per = (int64_t)kBS * kLeafItems;
-        hipLaunchKernelGGL(k_finalize, dim3(wb + (unsigned)((nleaf + per - 1) / per)), dim3(kBS), 0, st, ws->vis,
-                           nwords, ws->st, wb, ws->top1, ws->top1_flag, ws->leaf_lo, ws->leaf_lo + nleaf,
-                           (uint32_t)source, (uint32_t)level + 1u, ws->d_leafmax);
-    }
+    // unvisited (non-isolated) vertices -> WHITE; inside the timed region
+    hipLaunchKernelGGL(k_finalize, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->vis, nwords,
+                       ws->st);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
-    u64 leafmax = 0;
-    if (defer) BFSX_HIP_TRY(hipMemcpyAsync(&leafmax, ws->d_leafmax, sizeof(u64), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
-    if (defer) BFSX_HIP_TRY(hipStreamSynchronize(st));
     if (int e = check_queue_guard(ws)) return e;
-    const int core_levels = level + 1;
-    // a deferred vertex can sit one level beyond the core's deepest (the last pass expanded distance `level`
-    // and found nothing): the full BFS then has one more pass, which reached only deferred vertices (a
-    // record without kernels); k_finalize flags it
-    const int levels = core_levels + (leafmax ? 1 : 0);
+    ws->n_prec = n_prec;
+    ws->prec_nd.assign(rec_nd, rec_nd + n_prec);
+    ws->resolved = n_prec == 0;
+    const int levels = level + 1;
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
     g->level_cum_ms.resize(levels);
-    for (int l = 0; l < core_levels; l++) {
+    for (int l = 0; l < levels; l++) {
         float t = 0.f, k = 0.f;
         const LevelTiming &lt = timing[l];
         if (lt.persisted) { // device clock inside the launch that started at event slot lt.ev
@@ -3335,15 +3327,6 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         g->level_cum_ms[l] = t;
         g->level_stats[l].cum_ms = t;
         g->level_stats[l].kernel_ms = k;
-    }
-    if (levels > core_levels) {
-        bfsx_level_stat ls{};
-        ls.direction = BFSX_DIR_LEAVES;
-        ls.level = core_levels;
-        ls.cum_ms = ms;
-        g->level_stats.push_back(ls);
-        g->level_dirs.push_back(BFSX_DIR_LEAVES);
-        g->level_cum_ms[core_levels] = ms;
     }
     g->last_source = source;
     g->last_t_bfs_ms = ms;
@@ -3359,9 +3342,29 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
 
 } // namespace
 
+// Fold the last BFS's pull-level records into st (the validator's and m_comp's view of a result; outside
+// the timed region).  No-op when none is pending.
+int bfs_resolve(bfsx_graph *g) {
+    BfsWorkspace *ws = g->ws;
+    if (!ws || ws->resolved) return BFSX_OK;
+    hipStream_t st = g->ctx->stream;
+    RecSet rs{};
+    rs.n = ws->n_prec;
+    for (int r = 0; r < ws->n_prec; r++) {
+        rs.bm[r] = ws->prec[r];
+        rs.nd[r] = ws->prec_nd[r];
+    }
+    hipLaunchKernelGGL(k_resolve, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, rs,
+                       ws->nwords, ws->par, ws->st);
+    BFSX_LAUNCHED(st);
+    ws->resolved = true;
+    return BFSX_OK;
+}
+
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached) {
     BfsWorkspace *ws = g->ws;
     hipStream_t st = g->ctx->stream;
+    if (int e = bfs_resolve(g)) return e;
     u64 h[2] = {0, 0};
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(u64), st));
     hipLaunchKernelGGL(k_mcomp, dim3(clamp_grid((g->nv + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->st,
@@ -3376,41 +3379,110 @@ int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached) {
 
 const unsigned long long *bfs_state(const bfsx_graph *g) { return g->ws ? g->ws->st : nullptr; }
 
+namespace {
+
+constexpr size_t kStageBytes = (size_t)32 << 20; // one pinned staging chunk of the result copy
+
+// Host threads of the result copy: the job's CPU share (OMP_NUM_THREADS, as the GPU box sets it), at most 16.
+int copy_threads() {
+    static const int n = [] {
+        int t = (int)std::thread::hardware_concurrency();
+        if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+            const int x = std::atoi(e);
+            if (x > 0) t = std::min(t > 0 ? t : x, x);
+        }
+        return std::max(1, std::min(t, 16));
+    }();
+    return n;
+}
+
+} // namespace
+
+// The result in the caller's ids: one unpack kernel (state + pending records -> parent << 32 | dist per original
+// id, or int32 dist only), then the D2H copy through two pinned 32 MiB chunks, each split by host threads into
+// dist (int32) and parent (int64, -1 = none) while the next chunk is in flight (a pageable copy plus one host
+// thread widening 67 M parents took 80 ms at scale 26).
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     BfsWorkspace *ws = g->ws;
     if (!ws || g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
     hipStream_t st = g->ctx->stream;
     const size_t nv = (size_t)g->nv;
-    // unpack into the result's own staging buffers, then D2H.  Round 2 staged it in the frontier queues
-    // qa / qb: a consumer reading past a queue's tail then met the previous result's distances
-    // (INT32_MAX, small ints) as vertex ids ("Wrong-result events").
-    if (!ws->out_dist) {
-        BFSX_HIP_TRY(hipMalloc(&ws->out_dist, std::max<size_t>(nv, 1) * sizeof(int32_t)));
-        BFSX_HIP_TRY(hipMalloc(&ws->out_par, std::max<size_t>(nv, 1) * sizeof(int32_t)));
+    if (!ws->out64) {
+        BFSX_HIP_TRY(hipMalloc(&ws->out64, std::max<size_t>(nv, 1) * sizeof(u64)));
         BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack0));
         BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack1));
     }
-    int32_t *d_dist = ws->out_dist, *d_par = ws->out_par;
+    RecSet rs{};
+    rs.n = ws->resolved ? 0 : ws->n_prec;
+    for (int r = 0; r < rs.n; r++) {
+        rs.bm[r] = ws->prec[r];
+        rs.nd[r] = ws->prec_nd[r];
+    }
+    // dist only (int32 words) when only dist is asked for; parent << 32 | dist otherwise, also when nothing is
+    // copied (a device-only materialisation of the whole result: bfsx_result with two null outputs)
+    const bool packed = parent_out != nullptr || dist_out == nullptr;
+    int32_t *d_dist_only = packed ? nullptr : reinterpret_cast<int32_t *>(ws->out64);
+    const dim3 grid(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192));
     BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack0, st));
     if (g->d_inv)
-        hipLaunchKernelGGL(k_unpack_relabel, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                           ws->st, g->d_inv, g->v_lo, (int64_t)nv, d_dist, d_par);
+        hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo, (int64_t)nv,
+                           ws->out64, d_dist_only);
     else
-        hipLaunchKernelGGL(k_unpack, dim3(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->st,
-                           (int64_t)nv, d_dist, d_par);
+        hipLaunchKernelGGL(k_unpack<false>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo,
+                           (int64_t)nv, ws->out64, d_dist_only);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack1, st));
-    if (dist_out) BFSX_HIP_TRY(hipMemcpyAsync(dist_out, d_dist, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    if (parent_out) {
-        // int32 device parents land in the upper half of the int64 output, then widen in place
-        // (0xFFFFFFFF = none -> -1)
-        int32_t *p32 = reinterpret_cast<int32_t *>(parent_out) + nv;
-        BFSX_HIP_TRY(hipMemcpyAsync(p32, d_par, nv * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
-        for (size_t i = 0; i < nv; i++) parent_out[i] = (int64_t)p32[i];
-    } else {
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
+    if (dist_out || parent_out) {
+        if (!ws->h_stage) {
+            BFSX_HIP_TRY(hipHostMalloc(&ws->h_stage, 2 * kStageBytes, hipHostMallocDefault));
+            BFSX_HIP_TRY(hipEventCreateWithFlags(&ws->ev_stage[0], hipEventDisableTiming));
+            BFSX_HIP_TRY(hipEventCreateWithFlags(&ws->ev_stage[1], hipEventDisableTiming));
+        }
+        const size_t esz = packed ? sizeof(u64) : sizeof(int32_t);
+        const size_t per = kStageBytes / esz; // elements per chunk
+        const size_t nchunk = (nv + per - 1) / per;
+        const char *src = reinterpret_cast<const char *>(ws->out64);
+        char *stage[2] = {reinterpret_cast<char *>(ws->h_stage), reinterpret_cast<char *>(ws->h_stage) + kStageBytes};
+        auto issue = [&](size_t c) -> int {
+            const size_t b = c * per, n = std::min(per, nv - b);
+            BFSX_HIP_TRY(hipMemcpyAsync(stage[c & 1], src + b * esz, n * esz, hipMemcpyDeviceToHost, st));
+            BFSX_HIP_TRY(hipEventRecord(ws->ev_stage[c & 1], st));
+            return BFSX_OK;
+        };
+        const int T = copy_threads();
+        std::vector<std::thread> pool;
+        pool.reserve(T);
+        if (int e = issue(0)) return e;
+        for (size_t c = 0; c < nchunk; c++) {
+            BFSX_HIP_TRY(hipEventSynchronize(ws->ev_stage[c & 1]));
+            // the chunk before this one is fully split (joined below), so its buffer takes chunk c + 1
+            if (c + 1 < nchunk)
+                if (int e = issue(c + 1)) return e;
+            const size_t b = c * per, n = std::min(per, nv - b);
+            const char *buf = stage[c & 1];
+            auto split = [&, b, buf](size_t lo, size_t hi) {
+                if (packed) {
+                    const u64 *x = reinterpret_cast<const u64 *>(buf);
+                    for (size_t i = lo; i < hi; i++) {
+                        const u64 w = x[i];
+                        if (dist_out) dist_out[b + i] = (int32_t)(uint32_t)w;
+                        parent_out[b + i] = (int64_t)(int32_t)(uint32_t)(w >> 32); // 0xFFFFFFFF (none) -> -1
+                    }
+                } else {
+                    std::memcpy(dist_out + b + lo, buf + lo * sizeof(int32_t), (hi - lo) * sizeof(int32_t));
+                }
+            };
+            const size_t step = (n + T - 1) / T;
+            for (int t = 1; t < T; t++) {
+                const size_t lo = std::min(n, (size_t)t * step), hi = std::min(n, lo + step);
+                if (lo < hi) pool.emplace_back(split, lo, hi);
+            }
+            split(0, std::min(n, step));
+            for (auto &th : pool) th.join();
+            pool.clear();
+        }
     }
+    BFSX_HIP_TRY(hipStreamSynchronize(st));
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_unpack0, ws->ev_unpack1));
     ws->last_unpack_ms = ms;
@@ -3501,6 +3573,8 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
                        ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_LAUNCHED(st);
     ws->prev_source = sl;
+    ws->n_prec = 0; // the partitioned loop stores packed states only (no pull-level records)
+    ws->resolved = true;
     ws->d_level = 0;
     ws->d_dir = BFSX_DIR_TOPDOWN;
     ws->d_in_queue = true;
@@ -3615,7 +3689,7 @@ int dist_frontier_slice(bfsx_graph *g, u64 *d_slice) {
 int dist_bu_step(bfsx_graph *g, const u64 *d_front_global) {
     BfsWorkspace *ws = g->ws;
     if (!ws) return fail(BFSX_E_ARG, "bfsx_dist_begin first");
-    if (int e = launch_bu<true>(g, ws, d_front_global, ws->d_level)) return e;
+    if (int e = launch_bu<true>(g, ws, d_front_global, ws->next, nullptr, ws->d_level)) return e;
     ws->d_dir = BFSX_DIR_BOTTOMUP;
     ws->d_in_queue = false;
     return BFSX_OK;
@@ -3663,8 +3737,7 @@ int dist_finish(bfsx_graph *g) {
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     {
         const unsigned wb = clamp_grid((ws->nwords + kBS - 1) / kBS, cap);
-        hipLaunchKernelGGL(k_finalize, dim3(wb), dim3(kBS), 0, st, ws->vis, ws->nwords, ws->st, wb, ws->top1, 0u,
-                           (int64_t)0, (int64_t)0, 0u, 0u, nullptr); // no deferred tail
+        hipLaunchKernelGGL(k_finalize, dim3(wb), dim3(kBS), 0, st, ws->vis, ws->nwords, ws->st);
     }
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
@@ -4001,7 +4074,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 ws->d_in_queue = false;
             }
             if (int e = cm->allgather(ws->front, ws->nwords, ws->fglob, st)) return e;
-            if (int e = launch_bu<false>(g, ws, ws->fglob, level)) return e; // m_f from m_u (below)
+            if (int e = launch_bu<false>(g, ws, ws->fglob, ws->next, nullptr, level)) return e; // m_f from m_u (below)
             bu_levels++;
         }
         if (int e = dist_level_close(g, ws, td, h, summed)) return e;

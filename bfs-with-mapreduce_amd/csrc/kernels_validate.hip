@@ -92,6 +92,7 @@ __global__ __launch_bounds__(kBS) void k_validate(const int64_t *__restrict__ ro
 
 int bfs_validate(bfsx_graph *g, int64_t source, const unsigned long long *stt, int64_t res[4]) {
     if (!stt) {
+        if (int e = bfs_resolve(g)) return e;
         stt = bfs_state(g);
         if (!stt || g->last_source < 0) return fail(BFSX_E_ARG, "no BFS result on this graph yet");
         if (source < 0) source = g->last_source;

@@ -51,9 +51,6 @@ extern "C" {
 #define BFSX_DIR_HYBRID 3   /* (level records only) pull from the frontier's hubs + push from its other vertices */
 #define BFSX_DIR_BOTTOMUP_SPARSE 4 /* (level records only) a pull level with few unvisited candidates, run by the
                                      * sparse pull kernel (which also queues the next push frontier) */
-#define BFSX_DIR_LEAVES 5 /* (level records only) the pass that reaches only deferred degree-1 vertices (option
-                           * leaf_defer): they are resolved from their one neighbour after the core levels, so
-                           * this record carries no kernels of its own */
 
 typedef struct bfsx_ctx bfsx_ctx;
 typedef struct bfsx_graph bfsx_graph;
@@ -141,14 +138,6 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 the hub list with 0xFF before every BFS), "test_overread" = int|off (that push level reads one
  *                 queue entry past its tail: the id guard must fail the BFS), "bu_force_spill" = on|off (the
  *                 partitioned pull kernel in a build that spills to scratch)
- *   "leaf_defer" = on|off (single device: the degree-1 tail of a graph's id space -- on a relabelled graph
- *                 the ids >= 1 + the last row with two or more entries -- stays out of the level loop: it
- *                 is pre-visited, push levels never claim it and pull levels skip its bitmap words; after the
- *                 last level each such vertex takes its one neighbour as parent and that neighbour's
- *                 distance + 1 (inside the timed region).  Distances, parents, the pass count and
- *                 bfsx_level_times are those of the full BFS; the per-level frontier counts of
- *                 bfsx_level_stats exclude the deferred vertices, and a final pass that reaches only them is
- *                 recorded as BFSX_DIR_LEAVES.  Default off)
  *   "big_degree", "big_cap" = int (partitioned graphs: the ids of degree > big_degree, at most big_cap per
  *                 rank, are all-gathered with their degrees at the first BFS, so every rank knows a source's
  *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS) */
@@ -197,7 +186,8 @@ int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots);
  * (min distance / darkest colour, :90-108), collect + termination test (:110-117).
  * dist_out / parent_out may be NULL (results stay on the device, e.g. inside a timed region). */
 int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats);
-/* Copy the most recent bfsx_bfs result of this graph to host (same layout as bfsx_bfs outputs). */
+/* Copy the most recent bfsx_bfs result of this graph to host (same layout as bfsx_bfs outputs).  Both outputs
+ * NULL: the result is materialised on the device only (the unpack kernel, timed by bfsx_last_unpack_ms). */
 int bfsx_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
 /* Device time of each level of the most recent bfsx_bfs, cumulative like the reference's
  * Stopwatch (BfsSpark.java:59,63,111-112).  Returns the number of levels written (<= cap). */
@@ -205,11 +195,16 @@ int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap);
 /* Device time (ms) of the most recent BFS of g: source init -> last level complete, the stats.t_bfs_ms
  * figure without the m_comp reduction bfsx_bfs performs when stats are requested (benchmark loops). */
 int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms);
-/* Device time (ms) of the unpack kernel of the most recent bfsx_bfs / bfsx_result copy: the packed per-vertex
- * state (internal, degree-ordered ids) -> the int32 dist and parent arrays in ORIGINAL ids that the outputs
- * promise.  It runs after t_bfs (outside the timed region), before the D2H copy; -1 if no copy ran yet. */
+/* BFS runs of g re-run without the persistent push kernel since g was built (a K3p grid barrier that timed
+ * out; each such BFS's t_bfs covers the aborted attempt too).  Per call: bfsx_stats.persist_retries. */
+int bfsx_persist_fallbacks(const bfsx_graph *g, int64_t *count);
+/* Device time (ms) of the unpack kernel of the most recent bfsx_bfs / bfsx_result copy: the per-vertex state
+ * (internal, degree-ordered ids; a pull level's discoveries as 4-B parents + its level record) -> one word per
+ * ORIGINAL id (parent, dist) that the outputs are split from.  It runs after t_bfs (outside the timed region),
+ * before the D2H copy; -1 if no copy ran yet. */
 int bfsx_last_unpack_ms(const bfsx_graph *g, double *ms);
-/* Per-level direction of the most recent bfsx_bfs (BFSX_DIR_TOPDOWN / BFSX_DIR_BOTTOMUP). */
+/* Per-level direction of the most recent bfsx_bfs: BFSX_DIR_TOPDOWN (1), BFSX_DIR_BOTTOMUP (2), BFSX_DIR_HYBRID (3)
+ * or BFSX_DIR_BOTTOMUP_SPARSE (4). */
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap);
 
 /* Per-level records of the most recent bfsx_bfs.  Returns the number written (<= cap). */

@@ -67,7 +67,7 @@ public final class BfsGpu {
     private static void run(long ctx, String problemFile) throws IOException {
         final long g = Bfsx.loadAlgs4(ctx, problemFile); // GraphFileUtil.convert (BfsSpark.java:55)
         try {
-            final int nv = Math.toIntExact(Bfsx.nv(g));
+            final int nv = Bfsx.checkedInt(Bfsx.nv(g));
             final List<Set<Integer>> neighbours = neighbourSets(problemFile, nv);
             final ByteBuffer dist = Bfsx.ints(nv), parent = Bfsx.longs(nv);
             write(problemFile + "_0", neighbours, null, null, 0); // the initial state (GraphFileUtil.java:68)

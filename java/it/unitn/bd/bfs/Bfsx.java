@@ -86,10 +86,17 @@ public final class Bfsx {
 
     // ---- helpers -------------------------------------------------------------------------------------
     public static ByteBuffer ints(long n) {
-        return ByteBuffer.allocateDirect(Math.toIntExact(n * 4)).order(ByteOrder.nativeOrder());
+        return ByteBuffer.allocateDirect(checkedInt(n * 4)).order(ByteOrder.nativeOrder());
     }
 
     public static ByteBuffer longs(long n) {
-        return ByteBuffer.allocateDirect(Math.toIntExact(n * 8)).order(ByteOrder.nativeOrder());
+        return ByteBuffer.allocateDirect(checkedInt(n * 8)).order(ByteOrder.nativeOrder());
+    }
+
+    /** long -> int, failing on overflow (Java 7: Math.toIntExact is Java 8, the reference targets 1.7, pom.xml:16). */
+    public static int checkedInt(long x) {
+        if (x < Integer.MIN_VALUE || x > Integer.MAX_VALUE)
+            throw new ArithmeticException("integer overflow: " + x);
+        return (int) x;
     }
 }

@@ -20,7 +20,10 @@ def bench():
 def test_bottom_up_level_bytes(bench):
     ls = {"direction": 2, "unvisited_in": 1000, "stage2": 100, "claims": 10, "walked": 50, "frontier_out": 600}
     nwords = 64
-    assert bench.level_bytes(ls, nwords) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 8 * 600
+    # single device: a discovery stores its 4-B parent (the level record gives the distance)
+    assert bench.level_bytes(ls, nwords) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 4 * 600
+    # partitioned loop: the packed 8-B state
+    assert bench.level_bytes(ls, nwords, found_bytes=8) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 8 * 600
 
 
 def test_top_down_level_bytes(bench):

@@ -288,6 +288,31 @@ def test_persistent_abort_falls_back(ctx, abort_at):
         ctx.set_option("persist_abort_at", "off")
 
 
+def test_persistent_abort_time_covers_both_attempts(ctx):
+    """t_bfs of a BFS whose K3p launch aborted covers the aborted attempt AND the re-run (round-3 verdict: the
+    re-run re-recorded the start event, so the aborted attempt's time fell out of t_bfs).  A 1,100-vertex path:
+    the launch aborts after 1,000 K3p levels (persist_abort_at), the re-run takes per-level launches; t_bfs must
+    exceed the per-level run alone (persist off) by about the 1,000 K3p levels' span.  The graph counts the
+    re-run in bfsx_persist_fallbacks (what bench.py reports over its timed loop)."""
+    nv = 1100
+    u, v = np.arange(nv - 1, dtype=np.uint32), np.arange(1, nv, dtype=np.uint32)
+    try:
+        with ctx.from_edges(nv, u, v) as g:
+            g.bfs_device_only(0)
+            k3p = g.level_times()[999]  # the first 1,000 levels inside K3p: the aborted attempt's share
+            ctx.set_option("persist", "off")
+            t_off = min(g.bfs_device_only(0) for _ in range(3))
+            ctx.set_option("persist", "on")
+            ctx.set_option("persist_abort_at", "1000")
+            f0 = g.persist_fallbacks()
+            t_ab = [g.bfs_device_only(0) for _ in range(3)]
+            assert g.persist_fallbacks() - f0 == 3
+            assert min(t_ab) > t_off + 0.5 * k3p, (t_ab, t_off, k3p)
+    finally:
+        ctx.set_option("persist_abort_at", "off")
+        ctx.set_option("persist", "on")
+
+
 def test_persist_blocks_changed_between_runs(ctx):
     """persist_blocks raised after a graph's first K3p launch: the launch keeps the grid it was set up
     with, and the entry bound (every slice fits its output segment) is checked against THAT grid."""
@@ -576,9 +601,6 @@ def test_leaf_skip(ctx):
     option on and off, on (a) a graph whose pull level hands a push level a frontier of leaves only
     (the push level's queue is empty and the pass still counts), (b) Kronecker graphs over many roots,
     with and without K3p and hybrid levels."""
-    # the level structure below is the full loop's: the degree-1 tail stays in it (leaf_defer off;
-    # tests/test_gpu_leaf_defer.py covers the deferred tail)
-    ctx.set_option("leaf_defer", "off")
     # (a) s - h - c_i (3,000) ; c_i - leaf_i for i < 1,000 ; 100,000 isolated ids (n/24 above 3,000)
     s, h = 0, 1
     c = 2 + np.arange(3000)
@@ -627,7 +649,6 @@ def test_leaf_skip(ctx):
         ctx.set_option("persist", "on")
         ctx.set_option("hybrid", "auto")
         ctx.set_option("leaf_skip", "on")
-        ctx.set_option("leaf_defer", "off")
 
 
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
