@@ -351,6 +351,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.test_overread = (int)x;
         return BFSX_OK;
     }
+    if (k == "check_retired") {
+        if (v == "on") ctx->opt.check_retired = true;
+        else if (v == "off") ctx->opt.check_retired = false;
+        else return fail(BFSX_E_ARG, "check_retired must be on|off");
+        return BFSX_OK;
+    }
     if (k == "leaf_skip") {
         if (v == "on") ctx->opt.leaf_skip = true;
         else if (v == "off") ctx->opt.leaf_skip = false;

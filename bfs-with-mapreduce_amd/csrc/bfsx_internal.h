@@ -59,6 +59,7 @@ struct Options {
     bool poison_queues = false; // test hook: fill the frontier queues and hub list with 0xFF before every BFS
     bool bu_force_spill = false; // diagnostic: the partitioned pull kernel in a spilling (8 waves/SIMD) build
     int test_overread = -1;     // test hook: that top-down level's kernels read one queue entry past the tail
+    bool check_retired = false; // test hook: the partitioned loop fails if a launch or exchange uses a retired buffer
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------

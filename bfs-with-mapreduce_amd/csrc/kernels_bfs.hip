@@ -19,8 +19,10 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <initializer_list>
 #include <thread>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -187,7 +189,11 @@ struct BfsWorkspace {
     // temporaries): freed with the workspace, never in the middle of the loop.  The ranks of an in-process
     // group share one device, and a hipFree issued by one rank while the others' kernels ran coincided with
     // device memory faults in those kernels ("Wrong-result events", event (b)).
-    std::vector<void *> retired;
+    struct Retired {
+        const void *p;
+        size_t bytes;
+    };
+    std::vector<Retired> retired;
 };
 
 namespace {
@@ -2926,7 +2932,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr, (void *)ws->out64})
         if (p) (void)hipFree(p);
-    for (void *p : ws->retired) (void)hipFree(p);
+    for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
     for (void *p : ws->prec) (void)hipFree(p);
     if (ws->par) (void)hipFree(ws->par);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
@@ -3618,7 +3624,7 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
     // remote pairs <= adjacency entries of the local frontier
     const int64_t need = std::max<int64_t>(ws->d_mf, 1);
     if (need > ws->remote_cap) {
-        if (ws->remote) ws->retired.push_back(ws->remote);
+        if (ws->remote) ws->retired.push_back({ws->remote, (size_t)ws->remote_cap * sizeof(u64)});
         ws->remote = nullptr;
         ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
         BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
@@ -3796,10 +3802,27 @@ void trace_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level) {
 
 int grow(BfsWorkspace *ws, u64 *&buf, int64_t &cap, int64_t need) {
     if (need <= cap) return BFSX_OK;
-    if (buf) ws->retired.push_back(buf); // freed with the workspace (see BfsWorkspace::retired)
+    if (buf) ws->retired.push_back({buf, (size_t)cap * sizeof(u64)}); // freed with the workspace (BfsWorkspace::retired)
     buf = nullptr;
     cap = std::max<int64_t>(need, cap + cap / 2);
     BFSX_HIP_TRY(hipMalloc(&buf, cap * sizeof(u64)));
+    return BFSX_OK;
+}
+
+// Option check_retired (test hook): fail when a buffer pointer the next launches or exchanges use lies inside a
+// retired buffer (BfsWorkspace::retired) -- the debug assertion behind DESIGN.md 4, event (b): no kernel
+// argument, copy source or LocalGroup posting of the partitioned loop refers to a replaced buffer.
+int check_live(const bfsx_graph *g, const BfsWorkspace *ws, int level, const char *where,
+               std::initializer_list<std::pair<const char *, const void *>> ptrs) {
+    if (!g->ctx->opt.check_retired) return BFSX_OK;
+    for (const auto &x : ptrs) {
+        const uintptr_t a = (uintptr_t)x.second;
+        if (!a) continue;
+        for (const auto &r : ws->retired)
+            if (a >= (uintptr_t)r.p && a < (uintptr_t)r.p + r.bytes)
+                return fail(BFSX_E_HIP, std::string("check_retired: ") + where + " at level " + std::to_string(level) +
+                                            " uses " + x.first + ", which lies inside a retired buffer");
+    }
     return BFSX_OK;
 }
 
@@ -3817,14 +3840,17 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
     // posts the count ~0, so that all ranks leave together with the same error.
     // the temporaries are retired into the workspace, not freed here (see BfsWorkspace::retired)
     struct Bufs {
-        std::vector<void *> &sink;
+        std::vector<BfsWorkspace::Retired> &sink;
+        size_t chunk, cap, P;
         uint32_t *slice = nullptr;
         u64 *sel = nullptr, *cnt = nullptr, *all = nullptr;
         ~Bufs() {
-            for (void *p : {(void *)slice, (void *)sel, (void *)cnt, (void *)all})
-                if (p) sink.push_back(p);
+            if (slice) sink.push_back({slice, chunk * sizeof(uint32_t)});
+            if (sel) sink.push_back({sel, cap * sizeof(u64)});
+            if (cnt) sink.push_back({cnt, (1 + kMaxRanks) * sizeof(u64)});
+            if (all) sink.push_back({all, P * cap * sizeof(u64)});
         }
-    } b{ws->retired};
+    } b{ws->retired, (size_t)g->chunk, (size_t)cap, (size_t)P};
     BFSX_HIP_TRY(hipMalloc(&b.cnt, (1 + kMaxRanks) * sizeof(u64)));
     bool ok = hipMalloc(&b.slice, g->chunk * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&b.sel, cap * sizeof(u64)) == hipSuccess &&
@@ -3996,7 +4022,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             // remote pairs <= adjacency entries of the local frontier
             const int64_t need = std::max<int64_t>(ws->d_mf, 1);
             if (need > ws->remote_cap) {
-                if (ws->remote) ws->retired.push_back(ws->remote);
+                if (ws->remote) ws->retired.push_back({ws->remote, (size_t)ws->remote_cap * sizeof(u64)});
                 ws->remote = nullptr;
                 ws->remote_cap = std::max<int64_t>(need, 2 * ws->remote_cap);
                 BFSX_HIP_TRY(hipMalloc(&ws->remote, ws->remote_cap * sizeof(u64)));
@@ -4026,6 +4052,11 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 plan_slots(P, slot, plan);
                 ro = P * slot; // candidate entries the claim kernel reads
             }
+            if (int e = check_live(g, ws, level, "push kernels",
+                                   {{"queue in", ws->qa}, {"queue out", ws->qb}, {"hubs", ws->hubs}, {"vis", ws->vis},
+                                    {"state", ws->st}, {"remote", pt.remote}, {"slot_out", pt.slot_out},
+                                    {"counters", ws->d_dist_ctr}, {"front", ws->front}}))
+                return e;
             if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, dmax_local, level, pt)) return e;
             if (!slot) {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
@@ -4042,6 +4073,9 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 ro = plan.recv_total;
                 if (int e = grow(ws, ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
             }
+            if (int e = check_live(g, ws, level, "pair exchange + claim",
+                                   {{"sendbuf", ws->sendbuf}, {"recvbuf", ws->recvbuf}, {"remote", ws->remote}}))
+                return e;
             if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
                                       plan.rcount.data(), plan.rdispl.data(), st))
                 return e;
@@ -4073,6 +4107,10 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 BFSX_LAUNCHED(st);
                 ws->d_in_queue = false;
             }
+            if (int e = check_live(g, ws, level, "frontier all-gather + pull kernel",
+                                   {{"front", ws->front}, {"fglob", ws->fglob}, {"next", ws->next}, {"vis", ws->vis},
+                                    {"state", ws->st}}))
+                return e;
             if (int e = cm->allgather(ws->front, ws->nwords, ws->fglob, st)) return e;
             if (int e = launch_bu<false>(g, ws, ws->fglob, ws->next, nullptr, level)) return e; // m_f from m_u (below)
             bu_levels++;

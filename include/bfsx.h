@@ -137,7 +137,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   Test hooks and diagnostics (not for production): "poison_queues" = on|off (fill the frontier queues and
  *                 the hub list with 0xFF before every BFS), "test_overread" = int|off (that push level reads one
  *                 queue entry past its tail: the id guard must fail the BFS), "bu_force_spill" = on|off (the
- *                 partitioned pull kernel in a build that spills to scratch)
+ *                 partitioned pull kernel in a build that spills to scratch), "check_retired" = on|off (the
+ *                 partitioned loop fails when a launch or exchange would use a replaced (retired) buffer)
  *   "big_degree", "big_cap" = int (partitioned graphs: the ids of degree > big_degree, at most big_cap per
  *                 rank, are all-gathered with their degrees at the first BFS, so every rank knows a source's
  *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS) */

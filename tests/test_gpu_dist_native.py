@@ -91,6 +91,29 @@ def test_native_group_random(bfsx, world, direction):
     check(nv, u, v, sources, out)
 
 
+@pytest.mark.parametrize("world,direction", [(2, "auto"), (2, "topdown"), (3, "auto"), (4, "bottomup")])
+def test_native_group_no_retired_buffer_referenced(bfsx, world, direction):
+    """DESIGN.md 4, event (b): with option check_retired, every launch group and exchange of the partitioned
+    loop checks its buffer pointers against the buffers retired so far (grown exchange buffers, the degree
+    list's temporaries) and fails the BFS on a hit.  Graphs whose frontiers grow level by level and several
+    sources per graph make the loop replace its remote / send / receive buffers mid-BFS; the same random
+    graphs as test_native_group_random, plus a Kronecker graph (counted exchanges, hub rows)."""
+    rng = np.random.default_rng(100 + world)
+    nv = 6000
+    u = rng.integers(0, nv, 5 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 5 * nv).astype(np.uint32)
+    sources = [0, 2999, 5999, 17]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, direction,
+                    options={"check_retired": "on", "slot_pairs": "64"})
+    check(nv, u, v, sources, out)
+    scale, seed = 14, 0xC4EC
+    ku, kv = O.kronecker(scale, 16, seed)
+    ksrc = [int(ku[0]), int(ku[999]), int(ku[4242])]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, seed=seed), ksrc, direction,
+                    options={"check_retired": "on"})
+    check(1 << scale, ku, kv, ksrc, out)
+
+
 @pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("world", [2, 4])
 def test_native_group_kronecker(bfsx, world, relabel):
