@@ -26,6 +26,7 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "bfsx_internal.h"
 #include "exchange_plan.h"
@@ -163,6 +164,12 @@ struct BfsWorkspace {
     int64_t persist_fallbacks = 0; // BFS runs re-run without K3p after a barrier abort
     double clock_khz = 100000.0; // device wall-clock rate
     u64 pub_seq = 0;
+    // propagation-blocking push (k_pb_*): counts / offsets of the (bucket, workgroup) runs, the pairs, scan storage
+    uint32_t *pb_counts = nullptr;
+    u64 *pb_offs = nullptr, *pb_pairs = nullptr;
+    int64_t pb_cap = 0;
+    void *pb_tmp = nullptr;
+    size_t pb_tmp_bytes = 0;
     u64 *d_cursor = nullptr;            // bitmap -> queue compaction cursor
     u64 *d_red = nullptr;               // reductions (m_comp, reached)
     int64_t prev_source = -1;
@@ -746,6 +753,184 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
     publish_if_last(cn, pub, seq);
     if (kDist) slot_headers_if_last(pt);
+}
+
+// ---- K3b: propagation-blocking push for wide hub levels (single device) ------------------------------
+// A wide push level whose edges sit in hub rows (a hub root's second level: ~1.6 K hubs, ~20 M edges, ~6 M
+// discoveries) costs k_td_hubs one random line per visited probe, claim and state store: consecutive entries
+// of a hub row are thousands of ids apart (~60 G lines/s).  Propagation blocking turns the
+// scattered accesses into streams:
+//   k_pb_bin<false>  every workgroup sweeps its equal share of the hub rows' edges (as k_td_hubs) and counts
+//                    their targets per id bucket (2^bits ids) in LDS -> counts[bucket][workgroup];
+//   exclusive scan   (rocPRIM) of the counts: every (bucket, workgroup) run gets its place, bucket-major;
+//   k_pb_bin<true>   the same sweep appends (target << 32 | parent) pairs to the workgroup's run of their
+//                    bucket (LDS cursors; a run is written by one workgroup within a short window, so L2
+//                    merges its lines);
+//   k_pb_claim       one workgroup per bucket: the bucket's visited words in LDS, its pairs streamed in and
+//                    claimed with LDS atomics (first pair wins), the winners' states stored inside the
+//                    bucket's id range, the visited words written back whole.
+// The low-degree frontier vertices stay in k_td (global claims), which runs before; k_pb_claim loads the
+// visited words after it.  Reference: the mapper's emission (BfsSpark.java:73-79) and the reducer's
+// min-merge (:90-108), as k_td.
+constexpr int kPbGrid = 512;    // workgroups of the two sweeps (the counts matrix is kPbGrid x buckets)
+constexpr int kPbMaxBits = 18;  // bucket of at most 2^18 ids: 32 KiB of visited words in LDS
+constexpr int kPbMaxBuckets = 4096;
+
+template <bool kScatter, class OffT>
+__global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
+                                                const uint32_t *__restrict__ hubs, LevelSlot *ring, int level,
+                                                uint32_t nrows, u64 *err, int bits, int nb,
+                                                uint32_t *__restrict__ counts, const u64 *__restrict__ offs,
+                                                u64 *__restrict__ pairs) {
+    LevelSlot *cn = ring + (level + 1) % 3;
+    __shared__ u64 s_scan[kHubBatch + 1];
+    __shared__ int64_t s_beg[kHubBatch];
+    __shared__ uint32_t s_u[kHubBatch];
+    __shared__ u64 s_tsum[kBS];
+    __shared__ u64 s_cur[kPbMaxBuckets]; // count (pass 1) / next free slot (pass 2) of every bucket
+    const unsigned tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
+    for (int i = tid; i < nb; i += kBS) s_cur[i] = kScatter ? offs[(size_t)i * G + b] : 0ull;
+    const uint32_t nh = (uint32_t)cn->nhub;
+    constexpr int kPer = kHubBatch / kBS;
+    u64 scanned = 0;
+    __syncthreads();
+    for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
+        const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
+        u64 d[kPer], local = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int idx = (int)tid * kPer + k;
+            d[k] = 0;
+            if (idx < hb) {
+                const uint32_t u = hubs[h0 + idx];
+                const bool ok = kScatter ? u < nrows : id_ok(u, nrows, err);
+                const int64_t bg = ok ? (int64_t)row_off[u] : 0;
+                d[k] = ok ? (u64)((int64_t)row_off[u + 1] - bg) : 0ull;
+                s_beg[idx] = bg;
+                s_u[idx] = ok ? u : 0u;
+            }
+            local += d[k];
+        }
+        s_tsum[tid] = local;
+        __syncthreads();
+        for (int off = 1; off < kBS; off <<= 1) {
+            const u64 add = tid >= (unsigned)off ? s_tsum[tid - off] : 0ull;
+            __syncthreads();
+            s_tsum[tid] += add;
+            __syncthreads();
+        }
+        u64 run = s_tsum[tid] - local;
+        const u64 total = s_tsum[kBS - 1];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int idx = (int)tid * kPer + k;
+            s_scan[idx] = (idx < hb) ? run : total;
+            run += d[k];
+        }
+        if (tid == 0) s_scan[kHubBatch] = total;
+        __syncthreads();
+        const u64 x_begin = total * b / G, x_end = total * (b + 1) / G;
+        if (tid == 0) scanned += x_end - x_begin;
+        for (u64 x0 = x_begin; x0 < x_end; x0 += (u64)kBS * kItems) {
+            uint32_t v[kItems], pu[kItems];
+            bool valid[kItems];
+#pragma unroll
+            for (int k = 0; k < kItems; k++) {
+                const u64 x = x0 + (u64)k * kBS + tid;
+                valid[k] = x < x_end;
+                v[k] = 0;
+                pu[k] = 0;
+                if (valid[k]) {
+                    int lo = 0, hi = hb - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (s_scan[mid] <= x) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    v[k] = col[s_beg[lo] + (int64_t)(x - s_scan[lo])];
+                    pu[k] = s_u[lo];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kItems; k++) {
+                if (!valid[k]) continue;
+                const uint32_t bk = v[k] >> bits;
+                if (kScatter) {
+                    const u64 pos = atomicAdd(&s_cur[bk], 1ull);
+                    pairs[pos] = ((u64)v[k] << 32) | pu[k];
+                } else {
+                    atomicAdd(&s_cur[bk], 1ull);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!kScatter) {
+        for (int i = tid; i < nb; i += kBS) counts[(size_t)i * G + b] = (uint32_t)s_cur[i];
+        if (b == 0 && tid == 0) counts[(size_t)nb * G] = 0u; // the scan's last entry: offs[nb * G] = the total
+        shard_add(cn, 0, 0, scanned, 0, 0);
+    }
+}
+
+// Phase 2: bucket b = ids [b << bits, (b + 1) << bits); its pairs are offs[b * G .. (b + 1) * G) (G = the sweeps'
+// grid).  Publishes the level (its last kernel).
+template <class OffT>
+__global__ __launch_bounds__(kBS) void k_pb_claim(const OffT *__restrict__ row_off, const u64 *__restrict__ pairs,
+                                                  const u64 *__restrict__ offs, int G, int bits, int64_t nwords,
+                                                  u64 *__restrict__ vis, u64 *__restrict__ stt,
+                                                  uint32_t *__restrict__ qout, LevelSlot *ring, int level, HubSet hs,
+                                                  Published *pub, u64 seq) {
+    LevelSlot *cn = ring + (level + 1) % 3;
+    __shared__ u64 s_vis[(1 << kPbMaxBits) / 64];
+    __shared__ BlockQueue q;
+    bq_init(q);
+    const unsigned tid = threadIdx.x, b = blockIdx.x;
+    const int64_t w0 = ((int64_t)b << bits) >> 6;
+    const int nw = (int)min<int64_t>((int64_t)1 << (bits - 6), nwords - w0);
+    for (int i = tid; i < nw; i += kBS) s_vis[i] = vis[w0 + i];
+    const u64 beg = offs[(size_t)b * G], end = offs[(size_t)(b + 1) * G];
+    const int32_t nd = level + 1;
+    const uint32_t vlo = (uint32_t)(w0 * 64);
+    u64 acc_mf = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0, claims = 0;
+    __syncthreads();
+    for (u64 i0 = beg; i0 < end; i0 += (u64)kBS * kItems) {
+        u64 pr[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            const u64 i = i0 + (u64)k * kBS + tid;
+            pr[k] = i < end ? pairs[i] : ~0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            bool win = false;
+            const uint32_t v = (uint32_t)(pr[k] >> 32);
+            if (pr[k] != ~0ull) {
+                claims++;
+                const uint32_t r = v - vlo;
+                const u64 bit = 1ull << (r & 63u);
+                if (!(s_vis[r >> 6] & bit)) win = !(atomicOr(&s_vis[r >> 6], bit) & bit);
+                if (win) {
+                    stt[v] = pack_state((uint32_t)pr[k], nd);
+                    const u64 dg = (u64)(row_off[v + 1] - row_off[v]);
+                    acc_mf += dg;
+                    acc_dmax = dg > acc_dmax ? dg : acc_dmax;
+                    if (is_hub(hs, v, dg)) {
+                        acc_mfh += dg;
+                        acc_nh += 1;
+                    }
+                }
+            }
+            bq_push(q, win, v);
+        }
+        __syncthreads();
+        if (q.n > BlockQueue::kCap - (uint32_t)(kBS * kItems)) bq_flush(q, qout, &cn->qtail);
+    }
+    __syncthreads();
+    for (int i = tid; i < nw; i += kBS) vis[w0 + i] = s_vis[i];
+    bq_flush(q, qout, &cn->qtail);
+    // top-down fields as k_td_hubs: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
+    shard_add(cn, 0, acc_mf, 0, claims, 0, acc_dmax, acc_mfh, acc_nh);
+    publish_if_last(cn, pub, seq);
 }
 
 // ---- K3p: persistent top-down for narrow frontiers --------------------------------------------------
@@ -2551,6 +2736,53 @@ HubSet hub_set(const BfsWorkspace *ws) {
 }
 bool has_hubs(const BfsWorkspace *ws) { return ws->hub_k > 0 || ws->hub_lim > 0; }
 
+// Propagation-blocking buffers for a level of up to mf hub edges: the (bucket, workgroup) count / offset matrix
+// (fixed: kPbMaxBuckets x kPbGrid), the scan's storage, the pairs (grown to the largest level seen, kept).
+int pb_setup(bfsx_graph *g, BfsWorkspace *ws, int64_t mf) {
+    hipStream_t st = g->ctx->stream;
+    if (!ws->pb_counts) {
+        const size_t n = (size_t)kPbMaxBuckets * kPbGrid + 1;
+        BFSX_HIP_TRY(hipMalloc(&ws->pb_counts, n * sizeof(uint32_t)));
+        BFSX_HIP_TRY(hipMalloc(&ws->pb_offs, n * sizeof(u64)));
+        BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, ws->pb_tmp_bytes, ws->pb_counts, ws->pb_offs, (u64)0, n,
+                                             rocprim::plus<u64>(), st));
+        BFSX_HIP_TRY(hipMalloc(&ws->pb_tmp, std::max<size_t>(ws->pb_tmp_bytes, 16)));
+    }
+    if (ws->pb_cap < mf) {
+        if (ws->pb_pairs) BFSX_HIP_TRY(hipFree(ws->pb_pairs)); // single device: nothing of the BFS uses it yet
+        ws->pb_pairs = nullptr;
+        ws->pb_cap = std::max<int64_t>(mf, ws->pb_cap + ws->pb_cap / 2);
+        BFSX_HIP_TRY(hipMalloc(&ws->pb_pairs, (size_t)ws->pb_cap * sizeof(u64)));
+    }
+    return BFSX_OK;
+}
+
+// The hub rows of the level (ws->hubs, their count on the device) by propagation blocking: count, scan, scatter,
+// claim.  The claim kernel publishes the level.
+template <class OffT>
+int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int level, HubSet hs, Published *pub, u64 seq) {
+    hipStream_t st = g->ctx->stream;
+    const int64_t n = ws->nwords * 64;
+    int lg = 0;
+    while (((int64_t)1 << lg) < n) lg++;
+    const int bits = std::min(kPbMaxBits, std::max(12, lg - 10));
+    const int nb = (int)((n + ((int64_t)1 << bits) - 1) >> bits);
+    if (nb > kPbMaxBuckets) return fail(BFSX_E_ARG, "propagation-blocking push: too many id buckets");
+    hipLaunchKernelGGL((k_pb_bin<false, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->ring,
+                       level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
+    BFSX_LAUNCHED(st);
+    size_t tb = ws->pb_tmp_bytes;
+    BFSX_HIP_TRY(rocprim::exclusive_scan(ws->pb_tmp, tb, ws->pb_counts, ws->pb_offs, (u64)0,
+                                         (size_t)nb * kPbGrid + 1, rocprim::plus<u64>(), st));
+    hipLaunchKernelGGL((k_pb_bin<true, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->ring,
+                       level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
+    BFSX_LAUNCHED(st);
+    hipLaunchKernelGGL(k_pb_claim<OffT>, dim3(nb), dim3(kBS), 0, st, row_off, ws->pb_pairs, ws->pb_offs, kPbGrid, bits,
+                       ws->nwords, ws->vis, ws->st, ws->qb, ws->ring, level, hs, pub, seq);
+    BFSX_LAUNCHED(st);
+    return BFSX_OK;
+}
+
 // dmax: largest degree in the frontier (< 0: unknown) -- the hub bin is skipped when no vertex exceeds
 // the hub degree
 // skip_hubs (hybrid level): frontier vertices of the hub domain are left to the bottom-up hub sweep.
@@ -2572,6 +2804,24 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     // slot mode: only the level's last push kernel writes the slot headers
     Part pt0 = pt;
     if (hubs) pt0.slot_arrive = nullptr;
+    // a wide single-device level sweeps its hub rows by propagation blocking (k_pb_*) instead of k_td_hubs
+    const int64_t pb_min = g->ctx->opt.pb_min_edges;
+    const bool pb = !kDist && hubs && !skip_hubs && pb_min > 0 && mf >= pb_min;
+    if (pb) {
+        if (int e = pb_setup(g, ws, mf)) return e;
+        if (ws->off32) {
+            hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa,
+                               (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz,
+                               hs, skip, nullptr, seq);
+            BFSX_LAUNCHED(st);
+            return launch_pb(g, ws, ws->off32, level, hs, pub, seq);
+        }
+        hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs,
+                           skip, nullptr, seq);
+        BFSX_LAUNCHED(st);
+        return launch_pb(g, ws, g->d_row_off, level, hs, pub, seq);
+    }
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
                            ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
@@ -2933,6 +3183,8 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->d_dist_ctr, (void *)ws->out64})
         if (p) (void)hipFree(p);
     for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
+    for (void *p : {(void *)ws->pb_counts, (void *)ws->pb_offs, (void *)ws->pb_pairs, ws->pb_tmp})
+        if (p) (void)hipFree(p);
     for (void *p : ws->prec) (void)hipFree(p);
     if (ws->par) (void)hipFree(ws->par);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
