@@ -651,9 +651,10 @@ def test_leaf_skip(ctx):
         ctx.set_option("leaf_skip", "on")
 
 
+@pytest.mark.parametrize("floor", ["0", "65536"])
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
 @pytest.mark.parametrize("sparse", ["1", "64", "off"])
-def test_sparse_pull_levels(ctx, direction, sparse):
+def test_sparse_pull_levels(ctx, direction, sparse, floor):
     """The sparse pull kernel (k_bu_sparse, direction 4 in the level records): bu_sparse=1 runs EVERY pull
     level in it, 64 (the default) the tail levels, off none.  Distances, pass counts and parents against the
     oracle over 10 Kronecker roots, the queues poisoned (the push level after a sparse one reads the queue
@@ -666,6 +667,7 @@ def test_sparse_pull_levels(ctx, direction, sparse):
         ctx.set_option("direction", direction)
         ctx.set_option("bu_sparse", sparse)
         ctx.set_option("poison_queues", "on")
+        ctx.set_option("pull_min_edges", floor)
         for skip in ("on", "off"):
             ctx.set_option("leaf_skip", skip)
             with ctx.kronecker(15, 16, 0x5A5E) as g:
@@ -674,10 +676,11 @@ def test_sparse_pull_levels(ctx, direction, sparse):
                     seen += sum(1 for d in g.level_dirs() if d == 4)
         if sparse == "off":
             assert seen == 0
-        else:
+        elif floor == "0" or direction == "bottomup":
             assert seen > 0
     finally:
-        for k, val in (("direction", "auto"), ("bu_sparse", "64"), ("poison_queues", "off"), ("leaf_skip", "on")):
+        for k, val in (("direction", "auto"), ("bu_sparse", "64"), ("poison_queues", "off"), ("leaf_skip", "on"),
+                       ("pull_min_edges", "0")):
             ctx.set_option(k, val)
 
 
@@ -696,8 +699,9 @@ def _star_of_hubs(nhub, fan, tail):
     return nv, np.concatenate(u).astype(np.uint32), np.concatenate(v).astype(np.uint32)
 
 
+@pytest.mark.parametrize("floor", ["0", "65536"])
 @pytest.mark.parametrize("dmax", ["2048", "64", "8"])
-def test_persistent_heavy_rows(ctx, dmax):
+def test_persistent_heavy_rows(ctx, dmax, floor):
     """K3p's heavy rows (round 3): a row longer than persist_dmax is swept by the whole grid at the next
     level (equal edge shares); the source enters as one.  Bit-exact against the oracle and against the
     per-level kernels (persist off): a source of 6,000 hubs (every workgroup's heavy region overflows at
@@ -709,6 +713,7 @@ def test_persistent_heavy_rows(ctx, dmax):
         ctx.set_option("persist_dmax", dmax)
         ctx.set_option("direction", "topdown")  # push levels only: every narrow level is a K3p candidate
         ctx.set_option("poison_queues", "on")
+        ctx.set_option("pull_min_edges", floor)
         for nv, u, v in cases:
             off, col = O.build_sets(nv, u, v)
             with ctx.from_edges(nv, u, v) as g:
@@ -724,7 +729,8 @@ def test_persistent_heavy_rows(ctx, dmax):
                     _, _, st = check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=False)
                     assert st["persist_retries"] == 0
     finally:
-        for k, val in (("persist_dmax", "512"), ("direction", "auto"), ("poison_queues", "off")):
+        for k, val in (("persist_dmax", "512"), ("direction", "auto"), ("poison_queues", "off"),
+                       ("pull_min_edges", "0")):
             ctx.set_option(k, val)
 
 

@@ -83,22 +83,27 @@ def test_round2_failing_sequence_poisoned(ctx):
             ctx.set_option(k, val)
 
 
+@pytest.mark.parametrize("floor", ["0", "65536"])
 @pytest.mark.parametrize("leaf_skip", ["on", "off"])
 @pytest.mark.parametrize("persist,hybrid", [("on", "auto"), ("off", "auto"), ("on", "force")])
-def test_poisoned_queues_kronecker(ctx, leaf_skip, persist, hybrid):
+def test_poisoned_queues_kronecker(ctx, leaf_skip, persist, hybrid, floor):
     """Every queue hand-off of the single-device loop (push -> push, K3p -> push, pull -> push with the leaf
-    skip's shortened queue, hybrid levels) under poisoned queues: bit-exact distances over 12 roots."""
+    skip's shortened queue, hybrid levels) under poisoned queues: bit-exact distances over 12 roots.  floor:
+    the push -> pull floor (pull_min_edges); 65,536 is the default the bench runs, under which K3p takes over
+    the sparse pull's queue."""
     ou, ov = O.kronecker(16, 16, 0x1EAF)
     nv = 1 << 16
     off, col = O.build_sets(nv, ou, ov)
     try:
-        for k, val in (("poison_queues", "on"), ("leaf_skip", leaf_skip), ("persist", persist), ("hybrid", hybrid)):
+        for k, val in (("poison_queues", "on"), ("leaf_skip", leaf_skip), ("persist", persist), ("hybrid", hybrid),
+                       ("pull_min_edges", floor)):
             ctx.set_option(k, val)
         with ctx.kronecker(16, 16, 0x1EAF) as g:
             for r in g.sample_roots(12, seed=5):
                 check_against_oracle(g, nv, off, col, int(r), ou, ov, mr=False)
     finally:
-        for k, val in (("poison_queues", "off"), ("leaf_skip", "on"), ("persist", "on"), ("hybrid", "auto")):
+        for k, val in (("poison_queues", "off"), ("leaf_skip", "on"), ("persist", "on"), ("hybrid", "auto"),
+                       ("pull_min_edges", "0")):
             ctx.set_option(k, val)
 
 
