@@ -112,7 +112,8 @@ def lib():
         L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_last_bfs_ms.argtypes = [_VP, C.POINTER(C.c_double)]
         L.bfsx_last_unpack_ms.argtypes = [_VP, C.POINTER(C.c_double)]
-        L.bfsx_persist_fallbacks.argtypes = [_VP, C.POINTER(C.c_int64)]
+        if hasattr(L, "bfsx_persist_fallbacks") or not os.environ.get("BFSX_LIB"):  # an older build (A/B) may lack it
+            L.bfsx_persist_fallbacks.argtypes = [_VP, C.POINTER(C.c_int64)]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
         L.bfsx_device_synchronize.argtypes = [_VP]
         I64P = C.POINTER(C.c_int64)
@@ -322,6 +323,8 @@ class Graph:
 
     def persist_fallbacks(self):
         """BFS runs of this graph re-run without K3p since it was built (bfsx_persist_fallbacks)."""
+        if not hasattr(lib(), "bfsx_persist_fallbacks"):  # BFSX_LIB names an older build (A/B timing)
+            return -1
         n = C.c_int64()
         _check(lib().bfsx_persist_fallbacks(self._h, C.byref(n)))
         return n.value

@@ -166,7 +166,8 @@ struct BfsWorkspace {
     u64 pub_seq = 0;
     // propagation-blocking push (k_pb_*): counts / offsets of the (bucket, workgroup) runs, the pairs, scan storage
     uint32_t *pb_counts = nullptr;
-    u64 *pb_offs = nullptr, *pb_pairs = nullptr;
+    u64 *pb_offs = nullptr, *pb_pairs = nullptr, *pb_items = nullptr; // items: 3 words per claim part, + count
+    int64_t pb_items_cap = 0;
     int64_t pb_cap = 0;
     void *pb_tmp = nullptr;
     size_t pb_tmp_bytes = 0;
@@ -766,19 +767,28 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
 //   k_pb_bin<true>   the same sweep appends (target << 32 | parent) pairs to the workgroup's run of their
 //                    bucket (LDS cursors; a run is written by one workgroup within a short window, so L2
 //                    merges its lines);
-//   k_pb_claim       one workgroup per bucket: the bucket's visited words in LDS, its pairs streamed in and
-//                    claimed with LDS atomics (first pair wins), the winners' states stored inside the
-//                    bucket's id range, the visited words written back whole.
+//   k_pb_plan        splits every bucket's pairs into parts of at most kPbPart (the hub rows' targets pile up
+//                    in the low-id buckets of a degree-ordered graph: one workgroup per bucket took 3.75 ms);
+//   k_pb_claim       one workgroup per part: the bucket's visited words in LDS, the part's pairs streamed in
+//                    and claimed with LDS atomics (first pair wins); a bucket of one part writes its visited
+//                    words back whole, a split bucket arbitrates its locally-first pairs with one device
+//                    atomic each on the (cache-resident) visited words of its range; the winners' states are
+//                    stored inside the bucket's id range.
+// Phase 1 drops targets whose visited bit is set in the first kPbPrefIds ids (the hubs every hub row reaches,
+// copied to LDS once per workgroup).
 // The low-degree frontier vertices stay in k_td (global claims), which runs before; k_pb_claim loads the
 // visited words after it.  Reference: the mapper's emission (BfsSpark.java:73-79) and the reducer's
 // min-merge (:90-108), as k_td.
 constexpr int kPbGrid = 512;    // workgroups of the two sweeps (the counts matrix is kPbGrid x buckets)
 constexpr int kPbMaxBits = 18;  // bucket of at most 2^18 ids: 32 KiB of visited words in LDS
 constexpr int kPbMaxBuckets = 4096;
+constexpr int kPbPart = 16384;  // pairs per claim part
+constexpr uint32_t kPbPrefIds = 1u << 16; // phase 1 drops visited targets below this id (LDS copy of their words)
 
 template <bool kScatter, class OffT>
 __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                                const uint32_t *__restrict__ hubs, LevelSlot *ring, int level,
+                                                const uint32_t *__restrict__ hubs, const u64 *__restrict__ vis,
+                                                int64_t nwords, LevelSlot *ring, int level,
                                                 uint32_t nrows, u64 *err, int bits, int nb,
                                                 uint32_t *__restrict__ counts, const u64 *__restrict__ offs,
                                                 u64 *__restrict__ pairs) {
@@ -788,8 +798,11 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
     __shared__ uint32_t s_u[kHubBatch];
     __shared__ u64 s_tsum[kBS];
     __shared__ u64 s_cur[kPbMaxBuckets]; // count (pass 1) / next free slot (pass 2) of every bucket
+    __shared__ u64 s_pv[kPbPrefIds / 64]; // visited words of the first kPbPrefIds ids (a target there already visited is dropped)
     const unsigned tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
     for (int i = tid; i < nb; i += kBS) s_cur[i] = kScatter ? offs[(size_t)i * G + b] : 0ull;
+    const int npv = (int)min<int64_t>(kPbPrefIds / 64, nwords);
+    for (int i = tid; i < npv; i += kBS) s_pv[i] = vis[i];
     const uint32_t nh = (uint32_t)cn->nhub;
     constexpr int kPer = kHubBatch / kBS;
     u64 scanned = 0;
@@ -854,6 +867,7 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
 #pragma unroll
             for (int k = 0; k < kItems; k++) {
                 if (!valid[k]) continue;
+                if (v[k] < (uint32_t)npv * 64u && ((s_pv[v[k] >> 6] >> (v[k] & 63u)) & 1ull)) continue;
                 const uint32_t bk = v[k] >> bits;
                 if (kScatter) {
                     const u64 pos = atomicAdd(&s_cur[bk], 1ull);
@@ -872,61 +886,110 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
     }
 }
 
-// Phase 2: bucket b = ids [b << bits, (b + 1) << bits); its pairs are offs[b * G .. (b + 1) * G) (G = the sweeps'
-// grid).  Publishes the level (its last kernel).
+// The claim parts: bucket b's pairs offs[b * G .. (b + 1) * G) (G = the sweeps' grid) cut into ceil(n / kPbPart)
+// parts (at least one).  items[i] = {pair begin, pair end, bucket | split << 31}; *nitems = their number.  One
+// workgroup.
+__global__ __launch_bounds__(kBS) void k_pb_plan(const u64 *__restrict__ offs, int G, int nb, u64 *__restrict__ items,
+                                                 u64 *__restrict__ nitems) {
+    __shared__ u64 s_wsum[kWaves];
+    __shared__ u64 s_base;
+    const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < nb; b0 += kBS) {
+        const int bk = b0 + (int)tid;
+        u64 lo = 0, n = 0, parts = 0;
+        if (bk < nb) {
+            lo = offs[(size_t)bk * G];
+            n = offs[(size_t)(bk + 1) * G] - lo;
+            parts = n ? (n + kPbPart - 1) / kPbPart : 0;
+        }
+        u64 incl = parts; // block inclusive scan of the part counts
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u64 y = __shfl_up(incl, d);
+            if (lane >= (unsigned)d) incl += y;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        u64 off = s_base + incl - parts;
+        for (int w = 0; w < (int)wave; w++) off += s_wsum[w];
+        for (u64 p = 0; p < parts; p++) {
+            const u64 plo = lo + p * kPbPart, phi = min(lo + n, plo + kPbPart);
+            items[3 * (off + p)] = plo;
+            items[3 * (off + p) + 1] = phi;
+            items[3 * (off + p) + 2] = (u64)bk | (parts > 1 ? (1ull << 31) : 0ull);
+        }
+        __syncthreads();
+        if (tid == kBS - 1) s_base = off + parts;
+        __syncthreads();
+    }
+    if (tid == 0) *nitems = s_base;
+}
+
+// Phase 2, one workgroup per part (items beyond *nitems: nothing to do).  Publishes the level (its last kernel).
 template <class OffT>
 __global__ __launch_bounds__(kBS) void k_pb_claim(const OffT *__restrict__ row_off, const u64 *__restrict__ pairs,
-                                                  const u64 *__restrict__ offs, int G, int bits, int64_t nwords,
-                                                  u64 *__restrict__ vis, u64 *__restrict__ stt,
-                                                  uint32_t *__restrict__ qout, LevelSlot *ring, int level, HubSet hs,
-                                                  Published *pub, u64 seq) {
+                                                  const u64 *__restrict__ items, const u64 *__restrict__ nitems,
+                                                  int bits, int64_t nwords, u64 *__restrict__ vis,
+                                                  u64 *__restrict__ stt, uint32_t *__restrict__ qout, LevelSlot *ring,
+                                                  int level, HubSet hs, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_vis[(1 << kPbMaxBits) / 64];
     __shared__ BlockQueue q;
     bq_init(q);
-    const unsigned tid = threadIdx.x, b = blockIdx.x;
-    const int64_t w0 = ((int64_t)b << bits) >> 6;
-    const int nw = (int)min<int64_t>((int64_t)1 << (bits - 6), nwords - w0);
-    for (int i = tid; i < nw; i += kBS) s_vis[i] = vis[w0 + i];
-    const u64 beg = offs[(size_t)b * G], end = offs[(size_t)(b + 1) * G];
-    const int32_t nd = level + 1;
-    const uint32_t vlo = (uint32_t)(w0 * 64);
+    const unsigned tid = threadIdx.x;
     u64 acc_mf = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0, claims = 0;
-    __syncthreads();
-    for (u64 i0 = beg; i0 < end; i0 += (u64)kBS * kItems) {
-        u64 pr[kItems];
+    if ((u64)blockIdx.x < *nitems) {
+        const u64 *it = items + 3 * (size_t)blockIdx.x;
+        const u64 beg = it[0], end = it[1];
+        const uint32_t bk = (uint32_t)it[2] & 0x7FFFFFFFu;
+        const bool split = (it[2] >> 31) & 1ull;
+        const int64_t w0 = ((int64_t)bk << bits) >> 6;
+        const int nw = (int)min<int64_t>((int64_t)1 << (bits - 6), nwords - w0);
+        for (int i = tid; i < nw; i += kBS) s_vis[i] = vis[w0 + i];
+        const int32_t nd = level + 1;
+        const uint32_t vlo = (uint32_t)(w0 * 64);
+        __syncthreads();
+        for (u64 i0 = beg; i0 < end; i0 += (u64)kBS * kItems) {
+            u64 pr[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; k++) {
-            const u64 i = i0 + (u64)k * kBS + tid;
-            pr[k] = i < end ? pairs[i] : ~0ull;
-        }
+            for (int k = 0; k < kItems; k++) {
+                const u64 i = i0 + (u64)k * kBS + tid;
+                pr[k] = i < end ? pairs[i] : ~0ull;
+            }
 #pragma unroll
-        for (int k = 0; k < kItems; k++) {
-            bool win = false;
-            const uint32_t v = (uint32_t)(pr[k] >> 32);
-            if (pr[k] != ~0ull) {
-                claims++;
-                const uint32_t r = v - vlo;
-                const u64 bit = 1ull << (r & 63u);
-                if (!(s_vis[r >> 6] & bit)) win = !(atomicOr(&s_vis[r >> 6], bit) & bit);
-                if (win) {
-                    stt[v] = pack_state((uint32_t)pr[k], nd);
-                    const u64 dg = (u64)(row_off[v + 1] - row_off[v]);
-                    acc_mf += dg;
-                    acc_dmax = dg > acc_dmax ? dg : acc_dmax;
-                    if (is_hub(hs, v, dg)) {
-                        acc_mfh += dg;
-                        acc_nh += 1;
+            for (int k = 0; k < kItems; k++) {
+                bool win = false;
+                const uint32_t v = (uint32_t)(pr[k] >> 32);
+                if (pr[k] != ~0ull) {
+                    claims++;
+                    const uint32_t r = v - vlo;
+                    const u64 bit = 1ull << (r & 63u);
+                    if (!(s_vis[r >> 6] & bit)) win = !(atomicOr(&s_vis[r >> 6], bit) & bit);
+                    // a split bucket: the other parts claim the same range, the device word decides
+                    if (win && split) win = !(atomicOr(vis + w0 + (r >> 6), bit) & bit);
+                    if (win) {
+                        stt[v] = pack_state((uint32_t)pr[k], nd);
+                        const u64 dg = (u64)(row_off[v + 1] - row_off[v]);
+                        acc_mf += dg;
+                        acc_dmax = dg > acc_dmax ? dg : acc_dmax;
+                        if (is_hub(hs, v, dg)) {
+                            acc_mfh += dg;
+                            acc_nh += 1;
+                        }
                     }
                 }
+                bq_push(q, win, v);
             }
-            bq_push(q, win, v);
+            __syncthreads();
+            if (q.n > BlockQueue::kCap - (uint32_t)(kBS * kItems)) bq_flush(q, qout, &cn->qtail);
         }
         __syncthreads();
-        if (q.n > BlockQueue::kCap - (uint32_t)(kBS * kItems)) bq_flush(q, qout, &cn->qtail);
+        if (!split)
+            for (int i = tid; i < nw; i += kBS) vis[w0 + i] = s_vis[i];
     }
     __syncthreads();
-    for (int i = tid; i < nw; i += kBS) vis[w0 + i] = s_vis[i];
     bq_flush(q, qout, &cn->qtail);
     // top-down fields as k_td_hubs: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
     shard_add(cn, 0, acc_mf, 0, claims, 0, acc_dmax, acc_mfh, acc_nh);
@@ -2750,9 +2813,13 @@ int pb_setup(bfsx_graph *g, BfsWorkspace *ws, int64_t mf) {
     }
     if (ws->pb_cap < mf) {
         if (ws->pb_pairs) BFSX_HIP_TRY(hipFree(ws->pb_pairs)); // single device: nothing of the BFS uses it yet
-        ws->pb_pairs = nullptr;
+        if (ws->pb_items) BFSX_HIP_TRY(hipFree(ws->pb_items));
+        ws->pb_pairs = ws->pb_items = nullptr;
         ws->pb_cap = std::max<int64_t>(mf, ws->pb_cap + ws->pb_cap / 2);
         BFSX_HIP_TRY(hipMalloc(&ws->pb_pairs, (size_t)ws->pb_cap * sizeof(u64)));
+        // parts: at most one per bucket plus one per kPbPart pairs
+        ws->pb_items_cap = kPbMaxBuckets + ws->pb_cap / kPbPart + 1;
+        BFSX_HIP_TRY(hipMalloc(&ws->pb_items, (size_t)(3 * ws->pb_items_cap + 1) * sizeof(u64)));
     }
     return BFSX_OK;
 }
@@ -2760,7 +2827,8 @@ int pb_setup(bfsx_graph *g, BfsWorkspace *ws, int64_t mf) {
 // The hub rows of the level (ws->hubs, their count on the device) by propagation blocking: count, scan, scatter,
 // claim.  The claim kernel publishes the level.
 template <class OffT>
-int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int level, HubSet hs, Published *pub, u64 seq) {
+int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int64_t mf, int level, HubSet hs, Published *pub,
+              u64 seq) {
     hipStream_t st = g->ctx->stream;
     const int64_t n = ws->nwords * 64;
     int lg = 0;
@@ -2768,16 +2836,23 @@ int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int level, H
     const int bits = std::min(kPbMaxBits, std::max(12, lg - 10));
     const int nb = (int)((n + ((int64_t)1 << bits) - 1) >> bits);
     if (nb > kPbMaxBuckets) return fail(BFSX_E_ARG, "propagation-blocking push: too many id buckets");
-    hipLaunchKernelGGL((k_pb_bin<false, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->ring,
-                       level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
+    hipLaunchKernelGGL((k_pb_bin<false, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
+                       ws->nwords, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs,
+                       ws->pb_pairs);
     BFSX_LAUNCHED(st);
     size_t tb = ws->pb_tmp_bytes;
     BFSX_HIP_TRY(rocprim::exclusive_scan(ws->pb_tmp, tb, ws->pb_counts, ws->pb_offs, (u64)0,
                                          (size_t)nb * kPbGrid + 1, rocprim::plus<u64>(), st));
-    hipLaunchKernelGGL((k_pb_bin<true, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->ring,
-                       level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
+    hipLaunchKernelGGL((k_pb_bin<true, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
+                       ws->nwords, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs,
+                       ws->pb_pairs);
     BFSX_LAUNCHED(st);
-    hipLaunchKernelGGL(k_pb_claim<OffT>, dim3(nb), dim3(kBS), 0, st, row_off, ws->pb_pairs, ws->pb_offs, kPbGrid, bits,
+    u64 *nitems = ws->pb_items + 3 * ws->pb_items_cap;
+    hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(kBS), 0, st, ws->pb_offs, kPbGrid, nb, ws->pb_items, nitems);
+    BFSX_LAUNCHED(st);
+    // the grid covers the largest plan the level can have (its hub edges are at most mf)
+    const unsigned gc = (unsigned)std::min<int64_t>(ws->pb_items_cap, nb + mf / kPbPart + 1);
+    hipLaunchKernelGGL(k_pb_claim<OffT>, dim3(gc), dim3(kBS), 0, st, row_off, ws->pb_pairs, ws->pb_items, nitems, bits,
                        ws->nwords, ws->vis, ws->st, ws->qb, ws->ring, level, hs, pub, seq);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
@@ -2814,13 +2889,13 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
                                (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz,
                                hs, skip, nullptr, seq);
             BFSX_LAUNCHED(st);
-            return launch_pb(g, ws, ws->off32, level, hs, pub, seq);
+            return launch_pb(g, ws, ws->off32, mf, level, hs, pub, seq);
         }
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs,
                            skip, nullptr, seq);
         BFSX_LAUNCHED(st);
-        return launch_pb(g, ws, g->d_row_off, level, hs, pub, seq);
+        return launch_pb(g, ws, g->d_row_off, mf, level, hs, pub, seq);
     }
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
@@ -3183,7 +3258,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->d_dist_ctr, (void *)ws->out64})
         if (p) (void)hipFree(p);
     for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
-    for (void *p : {(void *)ws->pb_counts, (void *)ws->pb_offs, (void *)ws->pb_pairs, ws->pb_tmp})
+    for (void *p : {(void *)ws->pb_counts, (void *)ws->pb_offs, (void *)ws->pb_pairs, (void *)ws->pb_items, ws->pb_tmp})
         if (p) (void)hipFree(p);
     for (void *p : ws->prec) (void)hipFree(p);
     if (ws->par) (void)hipFree(ws->par);
