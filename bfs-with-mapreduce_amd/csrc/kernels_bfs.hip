@@ -774,8 +774,9 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
 //                    words back whole, a split bucket arbitrates its locally-first pairs with one device
 //                    atomic each on the (cache-resident) visited words of its range; the winners' states are
 //                    stored inside the bucket's id range.
-// Phase 1 drops targets whose visited bit is set in the first kPbPrefIds ids (the hubs every hub row reaches,
-// copied to LDS once per workgroup).
+// Targets in the first kPbPrefIds ids (the hubs every hub row reaches: in a degree-ordered graph most of a hub
+// level's edges, piled onto a few KiB of visited words) are not binned: the counting sweep claims them directly
+// (probe + atomic, as k_td_hubs), after dropping the ones visited before the level (an LDS copy of their words).
 // The low-degree frontier vertices stay in k_td (global claims), which runs before; k_pb_claim loads the
 // visited words after it.  Reference: the mapper's emission (BfsSpark.java:73-79) and the reducer's
 // min-merge (:90-108), as k_td.
@@ -787,9 +788,9 @@ constexpr uint32_t kPbPrefIds = 1u << 16; // phase 1 drops visited targets below
 
 template <bool kScatter, class OffT>
 __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                                const uint32_t *__restrict__ hubs, const u64 *__restrict__ vis,
-                                                int64_t nwords, LevelSlot *ring, int level,
-                                                uint32_t nrows, u64 *err, int bits, int nb,
+                                                const uint32_t *__restrict__ hubs, u64 *vis, int64_t nwords,
+                                                u64 *__restrict__ stt, uint32_t *__restrict__ qout, HubSet hs,
+                                                LevelSlot *ring, int level, uint32_t nrows, u64 *err, int bits, int nb,
                                                 uint32_t *__restrict__ counts, const u64 *__restrict__ offs,
                                                 u64 *__restrict__ pairs) {
     LevelSlot *cn = ring + (level + 1) % 3;
@@ -798,14 +799,19 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
     __shared__ uint32_t s_u[kHubBatch];
     __shared__ u64 s_tsum[kBS];
     __shared__ u64 s_cur[kPbMaxBuckets]; // count (pass 1) / next free slot (pass 2) of every bucket
-    __shared__ u64 s_pv[kPbPrefIds / 64]; // visited words of the first kPbPrefIds ids (a target there already visited is dropped)
+    __shared__ u64 s_pv[kPbPrefIds / 64]; // visited words of the first kPbPrefIds ids, before the level
+    __shared__ typename std::conditional<kScatter, char, BlockQueue>::type q_storage;
+    BlockQueue *q = kScatter ? nullptr : reinterpret_cast<BlockQueue *>(&q_storage);
     const unsigned tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
     for (int i = tid; i < nb; i += kBS) s_cur[i] = kScatter ? offs[(size_t)i * G + b] : 0ull;
     const int npv = (int)min<int64_t>(kPbPrefIds / 64, nwords);
+    const uint32_t plim = (uint32_t)npv * 64u; // targets below it: claimed here (pass 1), never binned
     for (int i = tid; i < npv; i += kBS) s_pv[i] = vis[i];
+    if (!kScatter) bq_init(*q);
     const uint32_t nh = (uint32_t)cn->nhub;
+    const int32_t nd = level + 1;
     constexpr int kPer = kHubBatch / kBS;
-    u64 scanned = 0;
+    u64 scanned = 0, attempts = 0, acc_mf = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0;
     __syncthreads();
     for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
         const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
@@ -862,19 +868,42 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
                     }
                     v[k] = col[s_beg[lo] + (int64_t)(x - s_scan[lo])];
                     pu[k] = s_u[lo];
+                    // a target already visited before the level, inside the prefix: nothing to do in either pass
+                    if (v[k] < plim && ((s_pv[v[k] >> 6] >> (v[k] & 63u)) & 1ull)) valid[k] = false;
                 }
             }
 #pragma unroll
             for (int k = 0; k < kItems; k++) {
-                if (!valid[k]) continue;
-                if (v[k] < (uint32_t)npv * 64u && ((s_pv[v[k] >> 6] >> (v[k] & 63u)) & 1ull)) continue;
-                const uint32_t bk = v[k] >> bits;
                 if (kScatter) {
-                    const u64 pos = atomicAdd(&s_cur[bk], 1ull);
-                    pairs[pos] = ((u64)v[k] << 32) | pu[k];
+                    if (valid[k] && v[k] >= plim) {
+                        const u64 pos = atomicAdd(&s_cur[v[k] >> bits], 1ull);
+                        pairs[pos] = ((u64)v[k] << 32) | pu[k];
+                    }
                 } else {
-                    atomicAdd(&s_cur[bk], 1ull);
+                    // the prefix (the hubs every hub row reaches; their visited words and states are a few
+                    // cache-resident lines): claimed here as k_td_hubs claims; the rest is counted per bucket
+                    bool win = false;
+                    if (valid[k] && v[k] < plim) {
+                        win = claim(v[k], vis, attempts);
+                        if (win) {
+                            stt[v[k]] = pack_state(pu[k], nd);
+                            const u64 dg = (u64)(row_off[v[k] + 1] - row_off[v[k]]);
+                            acc_mf += dg;
+                            acc_dmax = dg > acc_dmax ? dg : acc_dmax;
+                            if (is_hub(hs, v[k], dg)) {
+                                acc_mfh += dg;
+                                acc_nh += 1;
+                            }
+                        }
+                    } else if (valid[k]) {
+                        atomicAdd(&s_cur[v[k] >> bits], 1ull);
+                    }
+                    bq_push(*q, win, v[k]);
                 }
+            }
+            if (!kScatter) {
+                __syncthreads();
+                if (q->n > BlockQueue::kCap - (uint32_t)(kBS * kItems)) bq_flush(*q, qout, &cn->qtail);
             }
         }
         __syncthreads();
@@ -882,7 +911,8 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
     if (!kScatter) {
         for (int i = tid; i < nb; i += kBS) counts[(size_t)i * G + b] = (uint32_t)s_cur[i];
         if (b == 0 && tid == 0) counts[(size_t)nb * G] = 0u; // the scan's last entry: offs[nb * G] = the total
-        shard_add(cn, 0, 0, scanned, 0, 0);
+        bq_flush(*q, qout, &cn->qtail);
+        shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
     }
 }
 
@@ -2837,15 +2867,15 @@ int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int64_t mf, 
     const int nb = (int)((n + ((int64_t)1 << bits) - 1) >> bits);
     if (nb > kPbMaxBuckets) return fail(BFSX_E_ARG, "propagation-blocking push: too many id buckets");
     hipLaunchKernelGGL((k_pb_bin<false, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
-                       ws->nwords, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs,
-                       ws->pb_pairs);
+                       ws->nwords, ws->st, ws->qb, hs, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb,
+                       ws->pb_counts, ws->pb_offs, ws->pb_pairs);
     BFSX_LAUNCHED(st);
     size_t tb = ws->pb_tmp_bytes;
     BFSX_HIP_TRY(rocprim::exclusive_scan(ws->pb_tmp, tb, ws->pb_counts, ws->pb_offs, (u64)0,
                                          (size_t)nb * kPbGrid + 1, rocprim::plus<u64>(), st));
     hipLaunchKernelGGL((k_pb_bin<true, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
-                       ws->nwords, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb, ws->pb_counts, ws->pb_offs,
-                       ws->pb_pairs);
+                       ws->nwords, ws->st, ws->qb, hs, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb,
+                       ws->pb_counts, ws->pb_offs, ws->pb_pairs);
     BFSX_LAUNCHED(st);
     u64 *nitems = ws->pb_items + 3 * ws->pb_items_cap;
     hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(kBS), 0, st, ws->pb_offs, kPbGrid, nb, ws->pb_items, nitems);

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 kernel trace of a short bench run (through gpurun): rocprofv3 --kernel-trace --stats, summary copied
+# to gpurun_out/<tag>/.  usage: bash tools/r04_prof.sh <tag> [bench args...]
+set -e -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-p1 "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
+find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+echo done > "$OUT/DONE"
