@@ -53,7 +53,7 @@ def level_bytes(ls, nwords, off_bytes=4, found_bytes=4):
     its device counters.  Frontier-bit and visited-bit probes are not counted (the n/8-byte bitmaps are
     cache-resident).  off_bytes: width of the row offsets the traversal kernels read (uint32 when the
     graph has < 2^32 adjacency entries).  found_bytes: the store of a pull level's discovery (4: the
-    single-device 4-B parent, whose distance is the level record; 8: the partitioned loop's packed state)."""
+    4-B parent, whose distance is the level's record bitmap; 8: a packed (parent, dist) state word)."""
     d = ls["direction"]
     if d in (2, 4):  # bottom-up (4: the sparse pull kernel of the tail levels, same accounting): visited word read + next word write, top1 of every live candidate, rest[]
         # (2nd..4th neighbours + degree, 16 B) of every top1 miss, the offset pair of each row walked past
@@ -502,7 +502,7 @@ def run_dist(args, world, rank, local_rank):
             g.dist_bfs(r, want_stats=False)
 
     off_bytes = 4 if g.nnz < 0xFFFFFFFF and "offset_bits=64" not in args.option else 8
-    acct = LevelAccount(part["chunk"] // 64, off_bytes, found_bytes=8)
+    acct = LevelAccount(part["chunk"] // 64, off_bytes)
     # The K steps run back to back between two barrier + device-synchronise brackets (the contract's
     # timed region); every BFS is collective, so the ranks stay in step through its RCCL calls.
     ctx.synchronize()

@@ -785,13 +785,14 @@ constexpr int kPbMaxBits = 18;  // bucket of at most 2^18 ids: 32 KiB of visited
 constexpr int kPbMaxBuckets = 4096;
 constexpr int kPbPart = 16384;  // pairs per claim part
 constexpr uint32_t kPbPrefIds = 1u << 16; // phase 1 drops visited targets below this id (LDS copy of their words)
+constexpr uint32_t kPbDirect = 1u << 20;  // targets below min(this, n / 64) are claimed directly, the rest binned
 
 template <bool kScatter, class OffT>
 __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                 const uint32_t *__restrict__ hubs, u64 *vis, int64_t nwords,
                                                 u64 *__restrict__ stt, uint32_t *__restrict__ qout, HubSet hs,
                                                 LevelSlot *ring, int level, uint32_t nrows, u64 *err, int bits, int nb,
-                                                uint32_t *__restrict__ counts, const u64 *__restrict__ offs,
+                                                uint32_t plim, uint32_t *__restrict__ counts, const u64 *__restrict__ offs,
                                                 u64 *__restrict__ pairs) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_scan[kHubBatch + 1];
@@ -805,7 +806,7 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
     const unsigned tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
     for (int i = tid; i < nb; i += kBS) s_cur[i] = kScatter ? offs[(size_t)i * G + b] : 0ull;
     const int npv = (int)min<int64_t>(kPbPrefIds / 64, nwords);
-    const uint32_t plim = (uint32_t)npv * 64u; // targets below it: claimed here (pass 1), never binned
+    const uint32_t pfx = (uint32_t)npv * 64u; // LDS-filtered prefix; targets below plim: claimed here (pass 1), never binned
     for (int i = tid; i < npv; i += kBS) s_pv[i] = vis[i];
     if (!kScatter) bq_init(*q);
     const uint32_t nh = (uint32_t)cn->nhub;
@@ -869,14 +870,14 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
                     v[k] = col[s_beg[lo] + (int64_t)(x - s_scan[lo])];
                     pu[k] = s_u[lo];
                     // a target already visited before the level, inside the prefix: nothing to do in either pass
-                    if (v[k] < plim && ((s_pv[v[k] >> 6] >> (v[k] & 63u)) & 1ull)) valid[k] = false;
+                    if (v[k] < pfx && ((s_pv[v[k] >> 6] >> (v[k] & 63u)) & 1ull)) valid[k] = false;
                 }
             }
 #pragma unroll
             for (int k = 0; k < kItems; k++) {
                 if (kScatter) {
                     if (valid[k] && v[k] >= plim) {
-                        const u64 pos = atomicAdd(&s_cur[v[k] >> bits], 1ull);
+                        const u64 pos = atomicAdd(&s_cur[(v[k] - plim) >> bits], 1ull);
                         pairs[pos] = ((u64)v[k] << 32) | pu[k];
                     }
                 } else {
@@ -896,7 +897,7 @@ __global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off
                             }
                         }
                     } else if (valid[k]) {
-                        atomicAdd(&s_cur[v[k] >> bits], 1ull);
+                        atomicAdd(&s_cur[(v[k] - plim) >> bits], 1ull);
                     }
                     bq_push(*q, win, v[k]);
                 }
@@ -961,7 +962,7 @@ __global__ __launch_bounds__(kBS) void k_pb_plan(const u64 *__restrict__ offs, i
 template <class OffT>
 __global__ __launch_bounds__(kBS) void k_pb_claim(const OffT *__restrict__ row_off, const u64 *__restrict__ pairs,
                                                   const u64 *__restrict__ items, const u64 *__restrict__ nitems,
-                                                  int bits, int64_t nwords, u64 *__restrict__ vis,
+                                                  int bits, uint32_t base, int64_t nwords, u64 *__restrict__ vis,
                                                   u64 *__restrict__ stt, uint32_t *__restrict__ qout, LevelSlot *ring,
                                                   int level, HubSet hs, Published *pub, u64 seq) {
     LevelSlot *cn = ring + (level + 1) % 3;
@@ -975,7 +976,7 @@ __global__ __launch_bounds__(kBS) void k_pb_claim(const OffT *__restrict__ row_o
         const u64 beg = it[0], end = it[1];
         const uint32_t bk = (uint32_t)it[2] & 0x7FFFFFFFu;
         const bool split = (it[2] >> 31) & 1ull;
-        const int64_t w0 = ((int64_t)bk << bits) >> 6;
+        const int64_t w0 = (((int64_t)bk << bits) + base) >> 6;
         const int nw = (int)min<int64_t>((int64_t)1 << (bits - 6), nwords - w0);
         for (int i = tid; i < nw; i += kBS) s_vis[i] = vis[w0 + i];
         const int32_t nd = level + 1;
@@ -2715,7 +2716,7 @@ int ws_alloc(bfsx_graph *g) {
     ws->nwords = g->chunk / 64;
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
     BFSX_HIP_TRY(hipMalloc(&ws->st, nv * sizeof(u64)));
-    if (g->nranks == 1) BFSX_HIP_TRY(hipMalloc(&ws->par, nv * sizeof(uint32_t)));
+    BFSX_HIP_TRY(hipMalloc(&ws->par, nv * sizeof(uint32_t)));
     BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(u64)));
@@ -2860,22 +2861,23 @@ template <class OffT>
 int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int64_t mf, int level, HubSet hs, Published *pub,
               u64 seq) {
     hipStream_t st = g->ctx->stream;
-    const int64_t n = ws->nwords * 64;
+    const int64_t base = std::min<int64_t>(kPbDirect, ws->nwords) & ~63ll; // binned targets: ids [base, n)
+    const int64_t n = ws->nwords * 64 - base;
     int lg = 0;
     while (((int64_t)1 << lg) < n) lg++;
-    const int bits = std::min(kPbMaxBits, std::max(12, lg - 10));
-    const int nb = (int)((n + ((int64_t)1 << bits) - 1) >> bits);
+    const int bits = std::min(kPbMaxBits, std::max(12, lg - 8));
+    const int nb = std::max<int>(1, (int)((n + ((int64_t)1 << bits) - 1) >> bits));
     if (nb > kPbMaxBuckets) return fail(BFSX_E_ARG, "propagation-blocking push: too many id buckets");
     hipLaunchKernelGGL((k_pb_bin<false, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
                        ws->nwords, ws->st, ws->qb, hs, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb,
-                       ws->pb_counts, ws->pb_offs, ws->pb_pairs);
+                       (uint32_t)base, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
     BFSX_LAUNCHED(st);
     size_t tb = ws->pb_tmp_bytes;
     BFSX_HIP_TRY(rocprim::exclusive_scan(ws->pb_tmp, tb, ws->pb_counts, ws->pb_offs, (u64)0,
                                          (size_t)nb * kPbGrid + 1, rocprim::plus<u64>(), st));
     hipLaunchKernelGGL((k_pb_bin<true, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
                        ws->nwords, ws->st, ws->qb, hs, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb,
-                       ws->pb_counts, ws->pb_offs, ws->pb_pairs);
+                       (uint32_t)base, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
     BFSX_LAUNCHED(st);
     u64 *nitems = ws->pb_items + 3 * ws->pb_items_cap;
     hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(kBS), 0, st, ws->pb_offs, kPbGrid, nb, ws->pb_items, nitems);
@@ -2883,7 +2885,7 @@ int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int64_t mf, 
     // the grid covers the largest plan the level can have (its hub edges are at most mf)
     const unsigned gc = (unsigned)std::min<int64_t>(ws->pb_items_cap, nb + mf / kPbPart + 1);
     hipLaunchKernelGGL(k_pb_claim<OffT>, dim3(gc), dim3(kBS), 0, st, row_off, ws->pb_pairs, ws->pb_items, nitems, bits,
-                       ws->nwords, ws->vis, ws->st, ws->qb, ws->ring, level, hs, pub, seq);
+                       (uint32_t)base, ws->nwords, ws->vis, ws->st, ws->qb, ws->ring, level, hs, pub, seq);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
@@ -3333,6 +3335,51 @@ int64_t bfs_persist_fallbacks(const bfsx_graph *g) { return g->ws ? g->ws->persi
 
 namespace {
 
+// The pull-level records of one BFS (BfsWorkspace::par): every pull level writes its discoveries into a fresh
+// bitmap of the pool; a BFS with more than kMaxRec pull levels folds them into st (k_resolve) and starts over.
+struct RecLog {
+    bfsx_graph *g;
+    BfsWorkspace *ws;
+    int n = 0;
+    int32_t nd[kMaxRec];
+    RecLog(bfsx_graph *g_, BfsWorkspace *ws_) : g(g_), ws(ws_) {
+        ws->n_prec = 0;
+        ws->resolved = true;
+    }
+    RecSet set() const {
+        RecSet rs{};
+        rs.n = n;
+        for (int r = 0; r < n; r++) {
+            rs.bm[r] = ws->prec[r];
+            rs.nd[r] = nd[r];
+        }
+        return rs;
+    }
+    // the record the next pull level writes (the frontier it reads, a former record, is never the one returned)
+    int take(u64 **out) {
+        hipStream_t st = g->ctx->stream;
+        if (n == kMaxRec) {
+            hipLaunchKernelGGL(k_resolve, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
+                               set(), ws->nwords, ws->par, ws->st);
+            BFSX_LAUNCHED(st);
+            n = 0;
+        }
+        while ((int)ws->prec.size() <= n) {
+            u64 *b = nullptr;
+            BFSX_HIP_TRY(hipMalloc(&b, ws->nwords * sizeof(u64)));
+            ws->prec.push_back(b);
+        }
+        *out = ws->prec[n];
+        return BFSX_OK;
+    }
+    void done(int32_t dist) { nd[n++] = dist; } // the record just written holds the vertices at distance dist
+    void finish() {
+        ws->n_prec = n;
+        ws->prec_nd.assign(nd, nd + n);
+        ws->resolved = n == 0;
+    }
+};
+
 int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_persist, bool record_start) {
     if (source < 0 || source >= g->nv)
         return fail(BFSX_E_RANGE, "source vertex " + std::to_string(source) + " outside [0, " +
@@ -3383,36 +3430,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int td_levels = 0, bu_levels = 0;
     // the bitmap frontier: ws->front after a push -> pull conversion, a pull level's record after a pull level
     const u64 *bmf = ws->front;
-    // pull-level records of this BFS (BfsWorkspace::par): every pull level writes its discoveries into a fresh
-    // one; a BFS with more than kMaxRec pull levels folds them into st (k_resolve) and starts over
-    int n_prec = 0;
-    int32_t rec_nd[kMaxRec];
-    ws->n_prec = 0;
-    ws->resolved = true;
-    auto rec_set = [&]() {
-        RecSet rs{};
-        rs.n = n_prec;
-        for (int r = 0; r < n_prec; r++) {
-            rs.bm[r] = ws->prec[r];
-            rs.nd[r] = rec_nd[r];
-        }
-        return rs;
-    };
-    auto take_rec = [&](u64 **out) -> int {
-        if (n_prec == kMaxRec) {
-            hipLaunchKernelGGL(k_resolve, dim3(clamp_grid((nwords * 64 + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                               rec_set(), nwords, ws->par, ws->st);
-            BFSX_LAUNCHED(st);
-            n_prec = 0; // the frontier (the last record) is read, not written, by the next pull level
-        }
-        while ((int)ws->prec.size() <= n_prec) {
-            u64 *b = nullptr;
-            BFSX_HIP_TRY(hipMalloc(&b, nwords * sizeof(u64)));
-            ws->prec.push_back(b);
-        }
-        *out = ws->prec[n_prec];
-        return BFSX_OK;
-    };
+    // pull-level records of this BFS (BfsWorkspace::par)
+    RecLog recs(g, ws);
     std::vector<LevelTiming> timing;
     g->level_dirs.clear();
     g->level_cum_ms.clear();
@@ -3455,7 +3474,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                                (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
             BFSX_LAUNCHED(st);
             u64 *rec = nullptr;
-            if (int e = take_rec(&rec)) return e;
+            if (int e = recs.take(&rec)) return e;
             if (int e = launch_bu_hubonly(g, ws, ws->front, rec, ws->par, level)) return e; // -> rec, vis, par
             const Part pt = single_part(g, ws);
             // -> qb; its winners also store their parent in par (they join the record below)
@@ -3496,7 +3515,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             in_queue = false;
             snapped = false;
             bu_levels++;
-            rec_nd[n_prec++] = level + 1;
+            recs.done(level + 1);
             bmf = rec;
             if (nf == 0) break;
             continue;
@@ -3603,7 +3622,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         } else {
             // few unvisited candidates (the tail levels): the sparse kernel, which also queues its discoveries
             sparse = opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - n_pre) * opt.bu_sparse <= nwords * 64;
-            if (int e = take_rec(&bu_rec)) return e;
+            if (int e = recs.take(&bu_rec)) return e;
             if (sparse) {
                 const uint32_t qlim = (uint32_t)(opt.leaf_skip ? std::min<int64_t>(ws->leaf_lo, nv) : nv);
                 if (int e = launch_bu_sparse(g, ws, bmf, bu_rec, ws->par, level, qlim, ws->d_pub, ++ws->pub_seq))
@@ -3657,7 +3676,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             mf = -1;   // not accumulated by the single-GPU bottom-up step
             dmax = -1;
             mfh = -1;
-            rec_nd[n_prec++] = level + 1;
+            recs.done(level + 1);
             bmf = bu_rec;
         }
         if (nf == 0) break;
@@ -3669,9 +3688,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     BFSX_HIP_TRY(hipEventRecord(ws->ev_end, st));
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
     if (int e = check_queue_guard(ws)) return e;
-    ws->n_prec = n_prec;
-    ws->prec_nd.assign(rec_nd, rec_nd + n_prec);
-    ws->resolved = n_prec == 0;
+    recs.finish();
     const int levels = level + 1;
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
@@ -4338,6 +4355,10 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     int64_t visited_local = owner ? 1 : 0;
     bool snapped = false; // ws->front holds the visited slice from before the last (top-down) level
     int td_levels = 0, bu_levels = 0;
+    // the local bitmap frontier: ws->front after a push -> pull conversion, the last pull level's record after a
+    // pull level; pull levels store 4-B parents plus their record, as on one device (RecLog, BfsWorkspace::par)
+    const u64 *bmf = ws->front;
+    RecLog recs(g, ws);
     ExchangePlan plan;
     std::vector<u64> hc(2 * kMaxRanks);
     for (;;) {
@@ -4365,7 +4386,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 const int64_t per_block_min = (int64_t)kBS * kCompactWords;
                 const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
                 const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
-                hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, ws->front, ws->nwords, wpb, ws->qa,
+                hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, bmf, ws->nwords, wpb, ws->qa,
                                    ws->d_cursor, ws->nwords * 64);
                 BFSX_LAUNCHED(st);
                 ws->d_in_queue = true;
@@ -4462,14 +4483,19 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                                        0, st, ws->qa, (uint32_t)ws->d_nf, ws->front, (uint32_t)g->nv, ws->d_err);
                 }
                 BFSX_LAUNCHED(st);
+                bmf = ws->front;
                 ws->d_in_queue = false;
             }
+            u64 *rec = nullptr;
+            if (int e = recs.take(&rec)) return e;
             if (int e = check_live(g, ws, level, "frontier all-gather + pull kernel",
-                                   {{"front", ws->front}, {"fglob", ws->fglob}, {"next", ws->next}, {"vis", ws->vis},
-                                    {"state", ws->st}}))
+                                   {{"front", bmf}, {"fglob", ws->fglob}, {"record", rec}, {"vis", ws->vis},
+                                    {"parents", ws->par}}))
                 return e;
-            if (int e = cm->allgather(ws->front, ws->nwords, ws->fglob, st)) return e;
-            if (int e = launch_bu<false>(g, ws, ws->fglob, ws->next, nullptr, level)) return e; // m_f from m_u (below)
+            if (int e = cm->allgather(bmf, ws->nwords, ws->fglob, st)) return e;
+            if (int e = launch_bu<false>(g, ws, ws->fglob, rec, ws->par, level)) return e; // m_f from m_u (below)
+            recs.done(level + 1);
+            bmf = rec;
             bu_levels++;
         }
         if (int e = dist_level_close(g, ws, td, h, summed)) return e;
@@ -4494,7 +4520,6 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         examined += h[3];
         visited_local += h[0];
         if (td) std::swap(ws->qa, ws->qb);
-        else std::swap(ws->front, ws->next);
         dmax_local = td ? h[7] : (h[11] == 0 ? (int64_t)opt.hub_degree : -1);
         ws->d_dir = dir;
         ws->d_in_queue = td;
@@ -4515,6 +4540,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         }
         if (nf == 0) break;
     }
+    recs.finish();
     if ((rc = dist_finish(g))) return rc;
     if (stats) {
         *stats = bfsx_stats{};
