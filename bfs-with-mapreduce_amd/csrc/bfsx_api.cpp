@@ -351,17 +351,6 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.test_overread = (int)x;
         return BFSX_OK;
     }
-    if (k == "pb_min_edges") {
-        if (v == "off") {
-            ctx->opt.pb_min_edges = 0;
-            return BFSX_OK;
-        }
-        char *end = nullptr;
-        const long long x = strtoll(value, &end, 10);
-        if (!end || *end || x < 0) return fail(BFSX_E_ARG, "pb_min_edges must be an integer >= 0 or off");
-        ctx->opt.pb_min_edges = x;
-        return BFSX_OK;
-    }
     if (k == "check_retired") {
         if (v == "on") ctx->opt.check_retired = true;
         else if (v == "off") ctx->opt.check_retired = false;

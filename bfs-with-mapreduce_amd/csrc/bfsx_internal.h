@@ -35,8 +35,6 @@ struct Options {
     int beta = 24;              // bottom-up -> top-down when n_f < n / beta (and shrinking)
     int64_t pull_min_edges = (int64_t)1 << 16; // push -> pull needs at least this many frontier edges (and n/512)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
-    int64_t pb_min_edges = (int64_t)1 << 22; // single device: push levels with at least this many frontier edges
-                                // sweep their hub rows by propagation blocking (k_pb_*); 0 = never
     bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
     int persist_blocks = 0;     // K3p workgroups (0: one per CU)
     int offset_bits = 0;        // traversal row-offset width: 0 = uint32 when nnz < 2^32, else int64; 64 = int64

@@ -26,7 +26,6 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 #include "bfsx_internal.h"
 #include "exchange_plan.h"
@@ -164,13 +163,6 @@ struct BfsWorkspace {
     int64_t persist_fallbacks = 0; // BFS runs re-run without K3p after a barrier abort
     double clock_khz = 100000.0; // device wall-clock rate
     u64 pub_seq = 0;
-    // propagation-blocking push (k_pb_*): counts / offsets of the (bucket, workgroup) runs, the pairs, scan storage
-    uint32_t *pb_counts = nullptr;
-    u64 *pb_offs = nullptr, *pb_pairs = nullptr, *pb_items = nullptr; // items: 3 words per claim part, + count
-    int64_t pb_items_cap = 0;
-    int64_t pb_cap = 0;
-    void *pb_tmp = nullptr;
-    size_t pb_tmp_bytes = 0;
     u64 *d_cursor = nullptr;            // bitmap -> queue compaction cursor
     u64 *d_red = nullptr;               // reductions (m_comp, reached)
     int64_t prev_source = -1;
@@ -754,277 +746,6 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
     publish_if_last(cn, pub, seq);
     if (kDist) slot_headers_if_last(pt);
-}
-
-// ---- K3b: propagation-blocking push for wide hub levels (single device) ------------------------------
-// A wide push level whose edges sit in hub rows (a hub root's second level: ~1.6 K hubs, ~20 M edges, ~6 M
-// discoveries) costs k_td_hubs one random line per visited probe, claim and state store: consecutive entries
-// of a hub row are thousands of ids apart (~60 G lines/s).  Propagation blocking turns the
-// scattered accesses into streams:
-//   k_pb_bin<false>  every workgroup sweeps its equal share of the hub rows' edges (as k_td_hubs) and counts
-//                    their targets per id bucket (2^bits ids) in LDS -> counts[bucket][workgroup];
-//   exclusive scan   (rocPRIM) of the counts: every (bucket, workgroup) run gets its place, bucket-major;
-//   k_pb_bin<true>   the same sweep appends (target << 32 | parent) pairs to the workgroup's run of their
-//                    bucket (LDS cursors; a run is written by one workgroup within a short window, so L2
-//                    merges its lines);
-//   k_pb_plan        splits every bucket's pairs into parts of at most kPbPart (the hub rows' targets pile up
-//                    in the low-id buckets of a degree-ordered graph: one workgroup per bucket took 3.75 ms);
-//   k_pb_claim       one workgroup per part: the bucket's visited words in LDS, the part's pairs streamed in
-//                    and claimed with LDS atomics (first pair wins); a bucket of one part writes its visited
-//                    words back whole, a split bucket arbitrates its locally-first pairs with one device
-//                    atomic each on the (cache-resident) visited words of its range; the winners' states are
-//                    stored inside the bucket's id range.
-// Targets in the first kPbPrefIds ids (the hubs every hub row reaches: in a degree-ordered graph most of a hub
-// level's edges, piled onto a few KiB of visited words) are not binned: the counting sweep claims them directly
-// (probe + atomic, as k_td_hubs), after dropping the ones visited before the level (an LDS copy of their words).
-// The low-degree frontier vertices stay in k_td (global claims), which runs before; k_pb_claim loads the
-// visited words after it.  Reference: the mapper's emission (BfsSpark.java:73-79) and the reducer's
-// min-merge (:90-108), as k_td.
-constexpr int kPbGrid = 512;    // workgroups of the two sweeps (the counts matrix is kPbGrid x buckets)
-constexpr int kPbMaxBits = 18;  // bucket of at most 2^18 ids: 32 KiB of visited words in LDS
-constexpr int kPbMaxBuckets = 4096;
-constexpr int kPbPart = 16384;  // pairs per claim part
-constexpr uint32_t kPbPrefIds = 1u << 16; // phase 1 drops visited targets below this id (LDS copy of their words)
-constexpr uint32_t kPbDirect = 1u << 20;  // targets below min(this, n / 64) are claimed directly, the rest binned
-
-template <bool kScatter, class OffT>
-__global__ __launch_bounds__(kBS) void k_pb_bin(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
-                                                const uint32_t *__restrict__ hubs, u64 *vis, int64_t nwords,
-                                                u64 *__restrict__ stt, uint32_t *__restrict__ qout, HubSet hs,
-                                                LevelSlot *ring, int level, uint32_t nrows, u64 *err, int bits, int nb,
-                                                uint32_t plim, uint32_t *__restrict__ counts, const u64 *__restrict__ offs,
-                                                u64 *__restrict__ pairs) {
-    LevelSlot *cn = ring + (level + 1) % 3;
-    __shared__ u64 s_scan[kHubBatch + 1];
-    __shared__ int64_t s_beg[kHubBatch];
-    __shared__ uint32_t s_u[kHubBatch];
-    __shared__ u64 s_tsum[kBS];
-    __shared__ u64 s_cur[kPbMaxBuckets]; // count (pass 1) / next free slot (pass 2) of every bucket
-    __shared__ u64 s_pv[kPbPrefIds / 64]; // visited words of the first kPbPrefIds ids, before the level
-    __shared__ typename std::conditional<kScatter, char, BlockQueue>::type q_storage;
-    BlockQueue *q = kScatter ? nullptr : reinterpret_cast<BlockQueue *>(&q_storage);
-    const unsigned tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
-    for (int i = tid; i < nb; i += kBS) s_cur[i] = kScatter ? offs[(size_t)i * G + b] : 0ull;
-    const int npv = (int)min<int64_t>(kPbPrefIds / 64, nwords);
-    const uint32_t pfx = (uint32_t)npv * 64u; // LDS-filtered prefix; targets below plim: claimed here (pass 1), never binned
-    for (int i = tid; i < npv; i += kBS) s_pv[i] = vis[i];
-    if (!kScatter) bq_init(*q);
-    const uint32_t nh = (uint32_t)cn->nhub;
-    const int32_t nd = level + 1;
-    constexpr int kPer = kHubBatch / kBS;
-    u64 scanned = 0, attempts = 0, acc_mf = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0;
-    __syncthreads();
-    for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
-        const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
-        u64 d[kPer], local = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int idx = (int)tid * kPer + k;
-            d[k] = 0;
-            if (idx < hb) {
-                const uint32_t u = hubs[h0 + idx];
-                const bool ok = kScatter ? u < nrows : id_ok(u, nrows, err);
-                const int64_t bg = ok ? (int64_t)row_off[u] : 0;
-                d[k] = ok ? (u64)((int64_t)row_off[u + 1] - bg) : 0ull;
-                s_beg[idx] = bg;
-                s_u[idx] = ok ? u : 0u;
-            }
-            local += d[k];
-        }
-        s_tsum[tid] = local;
-        __syncthreads();
-        for (int off = 1; off < kBS; off <<= 1) {
-            const u64 add = tid >= (unsigned)off ? s_tsum[tid - off] : 0ull;
-            __syncthreads();
-            s_tsum[tid] += add;
-            __syncthreads();
-        }
-        u64 run = s_tsum[tid] - local;
-        const u64 total = s_tsum[kBS - 1];
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int idx = (int)tid * kPer + k;
-            s_scan[idx] = (idx < hb) ? run : total;
-            run += d[k];
-        }
-        if (tid == 0) s_scan[kHubBatch] = total;
-        __syncthreads();
-        const u64 x_begin = total * b / G, x_end = total * (b + 1) / G;
-        if (tid == 0) scanned += x_end - x_begin;
-        for (u64 x0 = x_begin; x0 < x_end; x0 += (u64)kBS * kItems) {
-            uint32_t v[kItems], pu[kItems];
-            bool valid[kItems];
-#pragma unroll
-            for (int k = 0; k < kItems; k++) {
-                const u64 x = x0 + (u64)k * kBS + tid;
-                valid[k] = x < x_end;
-                v[k] = 0;
-                pu[k] = 0;
-                if (valid[k]) {
-                    int lo = 0, hi = hb - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (s_scan[mid] <= x) lo = mid;
-                        else hi = mid - 1;
-                    }
-                    v[k] = col[s_beg[lo] + (int64_t)(x - s_scan[lo])];
-                    pu[k] = s_u[lo];
-                    // a target already visited before the level, inside the prefix: nothing to do in either pass
-                    if (v[k] < pfx && ((s_pv[v[k] >> 6] >> (v[k] & 63u)) & 1ull)) valid[k] = false;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kItems; k++) {
-                if (kScatter) {
-                    if (valid[k] && v[k] >= plim) {
-                        const u64 pos = atomicAdd(&s_cur[(v[k] - plim) >> bits], 1ull);
-                        pairs[pos] = ((u64)v[k] << 32) | pu[k];
-                    }
-                } else {
-                    // the prefix (the hubs every hub row reaches; their visited words and states are a few
-                    // cache-resident lines): claimed here as k_td_hubs claims; the rest is counted per bucket
-                    bool win = false;
-                    if (valid[k] && v[k] < plim) {
-                        win = claim(v[k], vis, attempts);
-                        if (win) {
-                            stt[v[k]] = pack_state(pu[k], nd);
-                            const u64 dg = (u64)(row_off[v[k] + 1] - row_off[v[k]]);
-                            acc_mf += dg;
-                            acc_dmax = dg > acc_dmax ? dg : acc_dmax;
-                            if (is_hub(hs, v[k], dg)) {
-                                acc_mfh += dg;
-                                acc_nh += 1;
-                            }
-                        }
-                    } else if (valid[k]) {
-                        atomicAdd(&s_cur[(v[k] - plim) >> bits], 1ull);
-                    }
-                    bq_push(*q, win, v[k]);
-                }
-            }
-            if (!kScatter) {
-                __syncthreads();
-                if (q->n > BlockQueue::kCap - (uint32_t)(kBS * kItems)) bq_flush(*q, qout, &cn->qtail);
-            }
-        }
-        __syncthreads();
-    }
-    if (!kScatter) {
-        for (int i = tid; i < nb; i += kBS) counts[(size_t)i * G + b] = (uint32_t)s_cur[i];
-        if (b == 0 && tid == 0) counts[(size_t)nb * G] = 0u; // the scan's last entry: offs[nb * G] = the total
-        bq_flush(*q, qout, &cn->qtail);
-        shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
-    }
-}
-
-// The claim parts: bucket b's pairs offs[b * G .. (b + 1) * G) (G = the sweeps' grid) cut into ceil(n / kPbPart)
-// parts (at least one).  items[i] = {pair begin, pair end, bucket | split << 31}; *nitems = their number.  One
-// workgroup.
-__global__ __launch_bounds__(kBS) void k_pb_plan(const u64 *__restrict__ offs, int G, int nb, u64 *__restrict__ items,
-                                                 u64 *__restrict__ nitems) {
-    __shared__ u64 s_wsum[kWaves];
-    __shared__ u64 s_base;
-    const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    for (int b0 = 0; b0 < nb; b0 += kBS) {
-        const int bk = b0 + (int)tid;
-        u64 lo = 0, n = 0, parts = 0;
-        if (bk < nb) {
-            lo = offs[(size_t)bk * G];
-            n = offs[(size_t)(bk + 1) * G] - lo;
-            parts = n ? (n + kPbPart - 1) / kPbPart : 0;
-        }
-        u64 incl = parts; // block inclusive scan of the part counts
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const u64 y = __shfl_up(incl, d);
-            if (lane >= (unsigned)d) incl += y;
-        }
-        if (lane == 63) s_wsum[wave] = incl;
-        __syncthreads();
-        u64 off = s_base + incl - parts;
-        for (int w = 0; w < (int)wave; w++) off += s_wsum[w];
-        for (u64 p = 0; p < parts; p++) {
-            const u64 plo = lo + p * kPbPart, phi = min(lo + n, plo + kPbPart);
-            items[3 * (off + p)] = plo;
-            items[3 * (off + p) + 1] = phi;
-            items[3 * (off + p) + 2] = (u64)bk | (parts > 1 ? (1ull << 31) : 0ull);
-        }
-        __syncthreads();
-        if (tid == kBS - 1) s_base = off + parts;
-        __syncthreads();
-    }
-    if (tid == 0) *nitems = s_base;
-}
-
-// Phase 2, one workgroup per part (items beyond *nitems: nothing to do).  Publishes the level (its last kernel).
-template <class OffT>
-__global__ __launch_bounds__(kBS) void k_pb_claim(const OffT *__restrict__ row_off, const u64 *__restrict__ pairs,
-                                                  const u64 *__restrict__ items, const u64 *__restrict__ nitems,
-                                                  int bits, uint32_t base, int64_t nwords, u64 *__restrict__ vis,
-                                                  u64 *__restrict__ stt, uint32_t *__restrict__ qout, LevelSlot *ring,
-                                                  int level, HubSet hs, Published *pub, u64 seq) {
-    LevelSlot *cn = ring + (level + 1) % 3;
-    __shared__ u64 s_vis[(1 << kPbMaxBits) / 64];
-    __shared__ BlockQueue q;
-    bq_init(q);
-    const unsigned tid = threadIdx.x;
-    u64 acc_mf = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0, claims = 0;
-    if ((u64)blockIdx.x < *nitems) {
-        const u64 *it = items + 3 * (size_t)blockIdx.x;
-        const u64 beg = it[0], end = it[1];
-        const uint32_t bk = (uint32_t)it[2] & 0x7FFFFFFFu;
-        const bool split = (it[2] >> 31) & 1ull;
-        const int64_t w0 = (((int64_t)bk << bits) + base) >> 6;
-        const int nw = (int)min<int64_t>((int64_t)1 << (bits - 6), nwords - w0);
-        for (int i = tid; i < nw; i += kBS) s_vis[i] = vis[w0 + i];
-        const int32_t nd = level + 1;
-        const uint32_t vlo = (uint32_t)(w0 * 64);
-        __syncthreads();
-        for (u64 i0 = beg; i0 < end; i0 += (u64)kBS * kItems) {
-            u64 pr[kItems];
-#pragma unroll
-            for (int k = 0; k < kItems; k++) {
-                const u64 i = i0 + (u64)k * kBS + tid;
-                pr[k] = i < end ? pairs[i] : ~0ull;
-            }
-#pragma unroll
-            for (int k = 0; k < kItems; k++) {
-                bool win = false;
-                const uint32_t v = (uint32_t)(pr[k] >> 32);
-                if (pr[k] != ~0ull) {
-                    claims++;
-                    const uint32_t r = v - vlo;
-                    const u64 bit = 1ull << (r & 63u);
-                    if (!(s_vis[r >> 6] & bit)) win = !(atomicOr(&s_vis[r >> 6], bit) & bit);
-                    // a split bucket: the other parts claim the same range, the device word decides
-                    if (win && split) win = !(atomicOr(vis + w0 + (r >> 6), bit) & bit);
-                    if (win) {
-                        stt[v] = pack_state((uint32_t)pr[k], nd);
-                        const u64 dg = (u64)(row_off[v + 1] - row_off[v]);
-                        acc_mf += dg;
-                        acc_dmax = dg > acc_dmax ? dg : acc_dmax;
-                        if (is_hub(hs, v, dg)) {
-                            acc_mfh += dg;
-                            acc_nh += 1;
-                        }
-                    }
-                }
-                bq_push(q, win, v);
-            }
-            __syncthreads();
-            if (q.n > BlockQueue::kCap - (uint32_t)(kBS * kItems)) bq_flush(q, qout, &cn->qtail);
-        }
-        __syncthreads();
-        if (!split)
-            for (int i = tid; i < nw; i += kBS) vis[w0 + i] = s_vis[i];
-    }
-    __syncthreads();
-    bq_flush(q, qout, &cn->qtail);
-    // top-down fields as k_td_hubs: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
-    shard_add(cn, 0, acc_mf, 0, claims, 0, acc_dmax, acc_mfh, acc_nh);
-    publish_if_last(cn, pub, seq);
 }
 
 // ---- K3p: persistent top-down for narrow frontiers --------------------------------------------------
@@ -2830,66 +2551,6 @@ HubSet hub_set(const BfsWorkspace *ws) {
 }
 bool has_hubs(const BfsWorkspace *ws) { return ws->hub_k > 0 || ws->hub_lim > 0; }
 
-// Propagation-blocking buffers for a level of up to mf hub edges: the (bucket, workgroup) count / offset matrix
-// (fixed: kPbMaxBuckets x kPbGrid), the scan's storage, the pairs (grown to the largest level seen, kept).
-int pb_setup(bfsx_graph *g, BfsWorkspace *ws, int64_t mf) {
-    hipStream_t st = g->ctx->stream;
-    if (!ws->pb_counts) {
-        const size_t n = (size_t)kPbMaxBuckets * kPbGrid + 1;
-        BFSX_HIP_TRY(hipMalloc(&ws->pb_counts, n * sizeof(uint32_t)));
-        BFSX_HIP_TRY(hipMalloc(&ws->pb_offs, n * sizeof(u64)));
-        BFSX_HIP_TRY(rocprim::exclusive_scan(nullptr, ws->pb_tmp_bytes, ws->pb_counts, ws->pb_offs, (u64)0, n,
-                                             rocprim::plus<u64>(), st));
-        BFSX_HIP_TRY(hipMalloc(&ws->pb_tmp, std::max<size_t>(ws->pb_tmp_bytes, 16)));
-    }
-    if (ws->pb_cap < mf) {
-        if (ws->pb_pairs) BFSX_HIP_TRY(hipFree(ws->pb_pairs)); // single device: nothing of the BFS uses it yet
-        if (ws->pb_items) BFSX_HIP_TRY(hipFree(ws->pb_items));
-        ws->pb_pairs = ws->pb_items = nullptr;
-        ws->pb_cap = std::max<int64_t>(mf, ws->pb_cap + ws->pb_cap / 2);
-        BFSX_HIP_TRY(hipMalloc(&ws->pb_pairs, (size_t)ws->pb_cap * sizeof(u64)));
-        // parts: at most one per bucket plus one per kPbPart pairs
-        ws->pb_items_cap = kPbMaxBuckets + ws->pb_cap / kPbPart + 1;
-        BFSX_HIP_TRY(hipMalloc(&ws->pb_items, (size_t)(3 * ws->pb_items_cap + 1) * sizeof(u64)));
-    }
-    return BFSX_OK;
-}
-
-// The hub rows of the level (ws->hubs, their count on the device) by propagation blocking: count, scan, scatter,
-// claim.  The claim kernel publishes the level.
-template <class OffT>
-int launch_pb(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, int64_t mf, int level, HubSet hs, Published *pub,
-              u64 seq) {
-    hipStream_t st = g->ctx->stream;
-    const int64_t base = std::min<int64_t>(kPbDirect, ws->nwords) & ~63ll; // binned targets: ids [base, n)
-    const int64_t n = ws->nwords * 64 - base;
-    int lg = 0;
-    while (((int64_t)1 << lg) < n) lg++;
-    const int bits = std::min(kPbMaxBits, std::max(12, lg - 8));
-    const int nb = std::max<int>(1, (int)((n + ((int64_t)1 << bits) - 1) >> bits));
-    if (nb > kPbMaxBuckets) return fail(BFSX_E_ARG, "propagation-blocking push: too many id buckets");
-    hipLaunchKernelGGL((k_pb_bin<false, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
-                       ws->nwords, ws->st, ws->qb, hs, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb,
-                       (uint32_t)base, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
-    BFSX_LAUNCHED(st);
-    size_t tb = ws->pb_tmp_bytes;
-    BFSX_HIP_TRY(rocprim::exclusive_scan(ws->pb_tmp, tb, ws->pb_counts, ws->pb_offs, (u64)0,
-                                         (size_t)nb * kPbGrid + 1, rocprim::plus<u64>(), st));
-    hipLaunchKernelGGL((k_pb_bin<true, OffT>), dim3(kPbGrid), dim3(kBS), 0, st, row_off, g->d_col, ws->hubs, ws->vis,
-                       ws->nwords, ws->st, ws->qb, hs, ws->ring, level, (uint32_t)g->nv, ws->d_err, bits, nb,
-                       (uint32_t)base, ws->pb_counts, ws->pb_offs, ws->pb_pairs);
-    BFSX_LAUNCHED(st);
-    u64 *nitems = ws->pb_items + 3 * ws->pb_items_cap;
-    hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(kBS), 0, st, ws->pb_offs, kPbGrid, nb, ws->pb_items, nitems);
-    BFSX_LAUNCHED(st);
-    // the grid covers the largest plan the level can have (its hub edges are at most mf)
-    const unsigned gc = (unsigned)std::min<int64_t>(ws->pb_items_cap, nb + mf / kPbPart + 1);
-    hipLaunchKernelGGL(k_pb_claim<OffT>, dim3(gc), dim3(kBS), 0, st, row_off, ws->pb_pairs, ws->pb_items, nitems, bits,
-                       (uint32_t)base, ws->nwords, ws->vis, ws->st, ws->qb, ws->ring, level, hs, pub, seq);
-    BFSX_LAUNCHED(st);
-    return BFSX_OK;
-}
-
 // dmax: largest degree in the frontier (< 0: unknown) -- the hub bin is skipped when no vertex exceeds
 // the hub degree
 // skip_hubs (hybrid level): frontier vertices of the hub domain are left to the bottom-up hub sweep.
@@ -2911,24 +2572,6 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     // slot mode: only the level's last push kernel writes the slot headers
     Part pt0 = pt;
     if (hubs) pt0.slot_arrive = nullptr;
-    // a wide single-device level sweeps its hub rows by propagation blocking (k_pb_*) instead of k_td_hubs
-    const int64_t pb_min = g->ctx->opt.pb_min_edges;
-    const bool pb = !kDist && hubs && !skip_hubs && pb_min > 0 && mf >= pb_min;
-    if (pb) {
-        if (int e = pb_setup(g, ws, mf)) return e;
-        if (ws->off32) {
-            hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa,
-                               (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz,
-                               hs, skip, nullptr, seq);
-            BFSX_LAUNCHED(st);
-            return launch_pb(g, ws, ws->off32, mf, level, hs, pub, seq);
-        }
-        hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs,
-                           skip, nullptr, seq);
-        BFSX_LAUNCHED(st);
-        return launch_pb(g, ws, g->d_row_off, mf, level, hs, pub, seq);
-    }
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
                            ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
@@ -3290,8 +2933,6 @@ void bfs_workspace_free(BfsWorkspace *ws) {
                     (void *)ws->d_dist_ctr, (void *)ws->out64})
         if (p) (void)hipFree(p);
     for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
-    for (void *p : {(void *)ws->pb_counts, (void *)ws->pb_offs, (void *)ws->pb_pairs, (void *)ws->pb_items, ws->pb_tmp})
-        if (p) (void)hipFree(p);
     for (void *p : ws->prec) (void)hipFree(p);
     if (ws->par) (void)hipFree(ws->par);
     if (ws->h_err) (void)hipHostFree(ws->h_err);

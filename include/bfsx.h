@@ -130,9 +130,6 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 and its host wait; default 16384, 0 = never)
  *   "build_chunk" = int (CSR build: raw adjacency entries per sort/dedup chunk, default 2^30; bounds the
  *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device)
- *   "pb_min_edges" = int|off (single device: a push level whose frontier has at least this many edges sweeps
- *                 its hub rows by propagation blocking -- targets binned by id range, then claimed per range in
- *                 LDS -- instead of the multi-workgroup hub bin; default 4194304, 0/off never)
  *   "leaf_skip" = on|off (single device: the degree-1 vertices a pull level discovers stay out of the next
  *                 push level's queue -- their one neighbour is their parent; default on)
  *   "relabel" = on|off (graphs built after the call renumber their vertices by degree, descending, inside every

@@ -772,50 +772,3 @@ def test_level_stats_raw_matches(ctx):
             assert len(full) >= 2
             assert g.level_stats_decode(g.level_stats_raw(256)) == full
             assert g.level_stats_decode(g.level_stats_raw(1)) == full[:1]
-
-
-@pytest.mark.parametrize("direction", ["topdown", "auto"])
-@pytest.mark.parametrize("offsets", ["auto", "64"])
-def test_propagation_blocking_push(ctx, direction, offsets):
-    """Propagation-blocking push levels (k_pb_bin count / scan / scatter, k_pb_claim: the hub rows' targets
-    binned by id range, claimed per range in LDS).  pb_min_edges=1 sends every push level that has hub rows
-    through it, on a star forest with a hub of 5,000 leaves (one hub row, one bucket holding every target),
-    random graphs (many hubs, duplicate targets across rows, targets in every bucket) and Kronecker scales
-    12-16 (hub roots), with poisoned queues: distances and pass counts against the oracle, parents validated,
-    identical distances with the path off.  offsets=64: the int64 row-offset instantiation."""
-    cases = []
-    hub = 5000
-    u = np.r_[np.zeros(hub), np.arange(1, 200)].astype(np.uint32)
-    v = np.r_[np.arange(1, hub + 1), np.arange(hub + 1, hub + 200)].astype(np.uint32)
-    cases.append((hub + 200, u, v, [0, 7, hub + 5]))
-    rng = np.random.default_rng(99)
-    nv = 40000
-    ru = rng.integers(0, nv, 12 * nv).astype(np.uint32)
-    rv = (rng.pareto(1.2, 12 * nv) * 50).astype(np.int64) % nv
-    cases.append((nv, ru, rv.astype(np.uint32), [0, 1, 12345]))
-    try:
-        ctx.set_option("direction", direction)
-        ctx.set_option("offset_bits", offsets)
-        ctx.set_option("poison_queues", "on")
-        for nv, u, v, srcs in cases:
-            off, col = O.build_sets(nv, u, v)
-            res = {}
-            for pb in ("1", "off"):
-                ctx.set_option("pb_min_edges", pb)
-                with ctx.from_edges(nv, u, v) as g:
-                    for s in srcs:
-                        res.setdefault(s, []).append(check_against_oracle(g, nv, off, col, s, u, v, mr=False)[0])
-            for s in srcs:
-                assert np.array_equal(res[s][0], res[s][1])
-        for scale in (12, 16):
-            ku, kv = O.kronecker(scale, 16, 0xB10C)
-            n = 1 << scale
-            off, col = O.build_sets(n, ku, kv)
-            ctx.set_option("pb_min_edges", "1")
-            with ctx.kronecker(scale, 16, 0xB10C) as g:
-                for r in (int(x) for x in g.sample_roots(6, seed=3)):
-                    check_against_oracle(g, n, off, col, r, mr=False)
-    finally:
-        for k, val in (("direction", "auto"), ("offset_bits", "auto"), ("poison_queues", "off"),
-                       ("pb_min_edges", str(1 << 22))):
-            ctx.set_option(k, val)
