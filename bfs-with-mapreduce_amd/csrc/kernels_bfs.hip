@@ -136,6 +136,8 @@ struct BfsWorkspace {
     // not be result data and whose result data must not be frontier ids -- and two pinned host chunks the D2H
     // copy streams through while host threads split them into the caller's arrays
     u64 *out64 = nullptr;
+    int out_mode = 0;        // out64's fill: 0 none, 1 packed words, 2 int32 distances (isolated ids keep it)
+    int64_t out_dirty = -1;  // an isolated vertex whose out64 entry the last unpack overwrote (it was the source)
     u64 *h_stage = nullptr;
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_unpack0 = nullptr, ev_unpack1 = nullptr;
@@ -2102,12 +2104,16 @@ __global__ __launch_bounds__(kBS) void k_resolve(RecSet rs, int64_t nwords, cons
 // ORIGINAL id, out[o] = parent_original << 32 | dist (one scattered store per vertex where separate dist and
 // parent arrays took two), or dist only.  kRelabel: internal local row i is original vertex inv[lo + i] (a
 // partition's relabel keeps it inside the rank's range [lo, lo + n)); parents are global internal ids and map
-// back through the whole inv.
+// back through the whole inv.  Isolated vertices (`dead`; half the ids of a scale-26 Kronecker graph) keep
+// the unreached word the buffer was filled with once, except keep0 / keep1 (this BFS's source, the last one
+// written that was isolated), so only the other half costs a scattered store.
 template <bool kRelabel>
 __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
                                                 RecSet rs, const uint32_t *__restrict__ inv, int64_t lo, int64_t n,
+                                                const u64 *__restrict__ dead, int64_t keep0, int64_t keep1,
                                                 u64 *__restrict__ out, int32_t *__restrict__ dist_only) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        if (((dead[i >> 6] >> (i & 63)) & 1ull) && i != keep0 && i != keep1) continue;
         const u64 s = rec_state(stt, par, rs, i);
         const uint32_t o = kRelabel ? (uint32_t)((int64_t)inv[lo + i] - lo) : (uint32_t)i;
         if (dist_only) {
@@ -3444,14 +3450,36 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     const bool packed = parent_out != nullptr || dist_out == nullptr;
     int32_t *d_dist_only = packed ? nullptr : reinterpret_cast<int32_t *>(ws->out64);
     const dim3 grid(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192));
+    const int mode = packed ? 1 : 2;
+    if (ws->out_mode != mode) { // every entry unreached once; isolated vertices keep it from then on
+        if (packed) {
+            hipLaunchKernelGGL(k_fill64, grid, dim3(kBS), 0, st, ws->out64, (int64_t)nv, kUnreached);
+        } else {
+            hipLaunchKernelGGL(k_fill64, grid, dim3(kBS), 0, st, ws->out64, (int64_t)(nv + 1) / 2,
+                               ((u64)INT32_MAX << 32) | (u64)INT32_MAX);
+        }
+        BFSX_LAUNCHED(st);
+        ws->out_mode = mode;
+        ws->out_dirty = -1;
+    }
+    // the source's local row (a partition's non-owning ranks: none)
+    const int64_t src = (g->last_source >= g->v_lo && g->last_source < g->v_lo + g->nv) ? g->last_source - g->v_lo : -1;
+    bool src_dead = false; // an isolated source's entry must be reset by the next unpack
+    if (src >= 0) {
+        u64 dw = 0;
+        BFSX_HIP_TRY(hipMemcpyAsync(&dw, ws->dead + (src >> 6), sizeof(dw), hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        src_dead = (dw >> (src & 63)) & 1ull;
+    }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack0, st));
     if (g->d_inv)
         hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo, (int64_t)nv,
-                           ws->out64, d_dist_only);
+                           ws->dead, src, ws->out_dirty, ws->out64, d_dist_only);
     else
         hipLaunchKernelGGL(k_unpack<false>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo,
-                           (int64_t)nv, ws->out64, d_dist_only);
+                           (int64_t)nv, ws->dead, src, ws->out_dirty, ws->out64, d_dist_only);
     BFSX_LAUNCHED(st);
+    ws->out_dirty = src_dead ? src : -1;
     BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack1, st));
     if (dist_out || parent_out) {
         if (!ws->h_stage) {

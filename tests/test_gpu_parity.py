@@ -772,3 +772,31 @@ def test_level_stats_raw_matches(ctx):
             assert len(full) >= 2
             assert g.level_stats_decode(g.level_stats_raw(256)) == full
             assert g.level_stats_decode(g.level_stats_raw(1)) == full[:1]
+
+
+def test_result_copy_isolated_sources_and_modes(ctx):
+    """The result copy fills its staging once per mode and then skips isolated vertices (their entry stays
+    unreached); an isolated SOURCE is written and reset by the next copy.  Alternating isolated / connected
+    sources and the two copy modes (dist only: int32 staging; dist + parent: packed words) must always match the
+    oracle, and a device-only materialisation in between must not disturb the next copy."""
+    rng = np.random.default_rng(123)
+    nv = 30000
+    u = rng.integers(0, nv // 2, 4 * nv).astype(np.uint32)  # ids >= nv/2: isolated (most of them)
+    v = rng.integers(0, nv // 2, 4 * nv).astype(np.uint32)
+    u = np.r_[u, [nv - 7]].astype(np.uint32)  # a self-loop-only vertex
+    v = np.r_[v, [nv - 7]].astype(np.uint32)
+    off, col = O.build_sets(nv, u, v)
+    with ctx.from_edges(nv, u, v) as g:
+        for i, s in enumerate([nv - 1, 0, nv - 7, nv - 2, 5, nv - 1, 17]):
+            ref, _ = O.csr_bfs(nv, off, col, s)
+            if i % 3 == 2:
+                g.bfs_device_only(s)
+                g.unpack_device_only()
+                d, p = g.result(want_parent=True)
+            elif i % 3 == 1:
+                d, p, _ = g.bfs(s, want_parent=False)
+            else:
+                d, p, _ = g.bfs(s)
+            assert np.array_equal(d, ref), (i, s)
+            if p is not None:
+                assert O.validate(nv, off, col, s, d, p) == 0
