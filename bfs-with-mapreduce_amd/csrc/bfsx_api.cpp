@@ -351,6 +351,13 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.test_overread = (int)x;
         return BFSX_OK;
     }
+    if (k == "sparse_exchange") {
+        if (v == "off") ctx->opt.sparse_exchange = 0;
+        else if (v == "auto") ctx->opt.sparse_exchange = 1;
+        else if (v == "on") ctx->opt.sparse_exchange = 2;
+        else return fail(BFSX_E_ARG, "sparse_exchange must be auto|on|off");
+        return BFSX_OK;
+    }
     if (k == "check_retired") {
         if (v == "on") ctx->opt.check_retired = true;
         else if (v == "off") ctx->opt.check_retired = false;

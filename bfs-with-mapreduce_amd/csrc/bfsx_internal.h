@@ -60,6 +60,7 @@ struct Options {
     bool bu_force_spill = false; // diagnostic: the partitioned pull kernel in a spilling (8 waves/SIMD) build
     int test_overread = -1;     // test hook: that top-down level's kernels read one queue entry past the tail
     bool check_retired = false; // test hook: the partitioned loop fails if a launch or exchange uses a retired buffer
+    int sparse_exchange = 1;    // partitioned pull levels: small global frontiers exchanged as id lists (0 off, 1 auto, 2 on)
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------

@@ -9,6 +9,8 @@
 //   plan_counted   counts known (all-to-all of the per-destination counts): send/receive blocks packed
 //                  in rank order (the device bucketing scatters pairs to destination-ordered blocks)
 //   plan_slots     small levels: every peer gets a fixed slot [count, slot pairs] whatever it holds
+//   plan_broadcast a sparse frontier exchange: every rank sends its whole id list to every rank (itself
+//                  included) and receives every rank's list, packed in rank order
 //   alltoallv_ops  the point-to-point operations one rank issues for an all-to-allv (RcclComm: one
 //                  ncclSend/ncclRecv pair per peer inside a group, empty blocks skipped)
 #pragma once
@@ -52,6 +54,25 @@ inline void plan_slots(int P, int64_t slot, ExchangePlan &pl) {
     pl.rdispl.assign(P, 0);
     for (int p = 0; p < P; p++) pl.sdispl[p] = pl.rdispl[p] = (int64_t)p * (slot + 1);
     pl.send_total = pl.recv_total = (int64_t)P * (slot + 1);
+}
+
+// Sparse frontier exchange (a pull level whose global frontier is small): this rank's `mine` ids go to every
+// rank from offset 0; counts[p] = rank p's ids (the level close's all-reduced per-rank counts), received in rank
+// order -- the receive buffer then holds the whole global frontier as an id list.
+template <class U>
+inline void plan_broadcast(int P, int64_t mine, const U *counts, ExchangePlan &pl) {
+    pl.scount.assign(P, mine);
+    pl.sdispl.assign(P, 0);
+    pl.rcount.assign(P, 0);
+    pl.rdispl.assign(P, 0);
+    int64_t ro = 0;
+    for (int p = 0; p < P; p++) {
+        pl.rcount[p] = (int64_t)counts[p];
+        pl.rdispl[p] = ro;
+        ro += pl.rcount[p];
+    }
+    pl.send_total = mine;
+    pl.recv_total = ro;
 }
 
 // Word offset of candidate entry i of a received slot exchange, or -1 when entry i is past its peer's count.

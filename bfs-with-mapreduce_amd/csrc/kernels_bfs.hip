@@ -1238,12 +1238,14 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // Multi-GPU level close (k_level_sums below, or the last workgroup of k_claim_remote): the level's counter
 // shards summed into out[0..6] = local {n_f, m_f, m_u, scanned, rows/claims, stage2, walked}, out[8..10] = copy
 // of {n_f, m_f, m_u} (all-reduced in place), and the next level's exchange counters `ctr` zeroed.
-//   out[7] = local d_max of the produced frontier (top-down), out[11] = local vertices found below hub_row_lim
+//   out[7] = local d_max of the produced frontier (top-down) or local vertices found below hub_row_lim
 //   (bottom-up): either tells the next push level whether it needs the hub bin.
+//   out[11 + r], r < nranks: this rank's n_f in its own slot, 0 elsewhere -- all-reduced with out[8..10], every
+//   rank learns every rank's frontier size (the sparse frontier exchange's receive counts).
 // One wave (threads 0..63) of the calling workgroup; the shards are read with agent-scope loads, so a
 // last-arriving workgroup of the level's last kernel can run it (k_claim_remote) as well as k_level_sums.
 __device__ inline void level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
-                                  u64 *__restrict__ ctr, int nctr) {
+                                  u64 *__restrict__ ctr, int nctr, int rank, int nranks) {
     if (threadIdx.x >= 64) return;
     const unsigned lane = threadIdx.x;
     auto ld = [](const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1263,8 +1265,8 @@ __device__ inline void level_sums(const LevelSlot *__restrict__ slot, int topdow
     if (lane == 0) {
         for (int i = 0; i < 7; i++) out[i] = (int64_t)t[i];
         for (int i = 0; i < 3; i++) out[8 + i] = (int64_t)t[i];
-        out[7] = (int64_t)dmax;
-        out[11] = (int64_t)nhub;
+        out[7] = (int64_t)(topdown ? dmax : nhub);
+        for (int r = 0; r < nranks; r++) out[11 + r] = r == rank ? (int64_t)t[0] : 0;
     }
 }
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
@@ -1274,7 +1276,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
                                                       LevelSlot *ring, int level, uint32_t lo, u64 slot,
                                                       uint32_t nrows, u64 *err, int64_t *sums, u64 *ctr, int nctr,
-                                                      u64 *arrive) {
+                                                      u64 *arrive, int rank, int nranks) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ BlockQueue q;
     bq_init(q);
@@ -1320,7 +1322,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     if (threadIdx.x == 0)
         s_last = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
     __syncthreads();
-    if (s_last) level_sums(cn, 1, sums, ctr, nctr);
+    if (s_last) level_sums(cn, 1, sums, ctr, nctr, rank, nranks);
 }
 
 // Multi-GPU: stable bucketing of remote pairs by owning rank (P <= kMaxRanks).  Two passes over the
@@ -1330,7 +1332,8 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
 constexpr int kCtrHead = 2 + 2 * kMaxRanks; // zeroed per level (the last word: k_claim_remote's arrivals)
 constexpr int kCtrRecv = kCtrHead;
 constexpr int kCtrSums = kCtrHead + kMaxRanks;
-constexpr int kCtrWords = kCtrSums + 16;
+constexpr int kCtrSums16 = 16 + kMaxRanks; // level sums: [0..10] as level_sums writes them, [11, 11 + P) per-rank n_f
+constexpr int kCtrWords = kCtrSums + kCtrSums16;
 
 
 __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
@@ -2282,6 +2285,19 @@ __global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, cons
     }
 }
 
+// Sparse frontier exchange (partitioned pull levels): local row ids -> global ids (u64 words of the send
+// buffer), and the received global ids -> the global frontier bitmap (zeroed before).
+__global__ __launch_bounds__(kBS) void k_ids_global(const uint32_t *__restrict__ ids, u64 n, uint32_t lo,
+                                                    u64 *__restrict__ out) {
+    for (u64 i = (u64)blockIdx.x * kBS + threadIdx.x; i < n; i += (u64)gridDim.x * kBS) out[i] = (u64)ids[i] + lo;
+}
+__global__ __launch_bounds__(kBS) void k_ids_to_bitmap(const u64 *__restrict__ ids, u64 n, u64 *bm) {
+    for (u64 i = (u64)blockIdx.x * kBS + threadIdx.x; i < n; i += (u64)gridDim.x * kBS) {
+        const u64 v = ids[i];
+        atomicOr(bm + (v >> 6), 1ull << (v & 63u));
+    }
+}
+
 // Multi-GPU host reads without a D2H copy + stream synchronise: one wave copies two device ranges into
 // mapped pinned host memory and then publishes a sequence number the host spins on (as publish_if_last).
 __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict__ b, int nb, u64 *post, u64 seq) {
@@ -2296,8 +2312,8 @@ __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict_
 // (the copy is all-reduced in place; the local half stays for the per-level record), and zeroes the
 // next top-down level's exchange counters `ctr` (nothing reads them after this level's claim kernel).
 __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
-                             u64 *__restrict__ ctr, int nctr) {
-    level_sums(slot, topdown, out, ctr, nctr);
+                             u64 *__restrict__ ctr, int nctr, int rank, int nranks) {
+    level_sums(slot, topdown, out, ctr, nctr, rank, nranks);
 }
 
 unsigned clamp_grid(int64_t blocks, unsigned cap) {
@@ -3707,11 +3723,11 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     if (ws->off32)
         hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, ws->off32, ws->vis,
                            ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
-                           nullptr, nullptr, 0, nullptr);
+                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks);
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
                            ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
-                           nullptr, nullptr, 0, nullptr);
+                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
@@ -3945,18 +3961,28 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
 }
 
 // level close: local sums + all-reduce of (n_f, m_f, m_u); returns [0..4] local, [8..10] global
-int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[16], bool summed) {
+int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[kCtrSums16], bool summed) {
     hipStream_t st = g->ctx->stream;
     const int level = ws->d_level;
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
     if (!summed) {
         hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums,
-                           ws->d_dist_ctr, kCtrHead);
+                           ws->d_dist_ctr, kCtrHead, g->rank, g->nranks);
         BFSX_LAUNCHED(st);
     }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-    if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3, st)) return e;
-    return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 16, nullptr, 0, reinterpret_cast<u64 *>(out));
+    if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3 + g->nranks, st)) return e;
+    return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 11 + g->nranks, nullptr, 0,
+                     reinterpret_cast<u64 *>(out));
+}
+
+// Option sparse_exchange: a pull level's global frontier travels as an id list when it holds fewer than n/128
+// vertices (auto; 8 B per id against the n/8-byte bitmap all-gather), always (on, P > 1) or never (off).  The
+// per-rank sizes come from the last level close; identical on every rank.
+bool sparse_exchange(const bfsx_graph *g, int64_t nf_global, const std::vector<int64_t> &rank_nf) {
+    const int mode = g->ctx->opt.sparse_exchange;
+    if (g->nranks < 2 || mode == 0 || (int)rank_nf.size() != g->nranks) return false;
+    return mode == 2 || nf_global * 128 < g->nv_global;
 }
 
 } // namespace
@@ -3976,7 +4002,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
     if (int e = grow(ws, ws->fglob, ws->fglob_words, ws->nwords * P)) return e;
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
-    int64_t h[16];
+    int64_t h[kCtrSums16];
     if (ws->nnz_global < 0) { // once per graph
         h[0] = g->nnz;
         BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -4028,6 +4054,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     // pull level; pull levels store 4-B parents plus their record, as on one device (RecLog, BfsWorkspace::par)
     const u64 *bmf = ws->front;
     RecLog recs(g, ws);
+    std::vector<int64_t> rank_nf; // every rank's frontier size after the last level close (all-reduced)
     ExchangePlan plan;
     std::vector<u64> hc(2 * kMaxRanks);
     for (;;) {
@@ -4132,15 +4159,60 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (ws->off32)
                     hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive);
+                                       (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive,
+                                       g->rank, g->nranks);
                 else
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
-                                       (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive);
+                                       (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive,
+                                       g->rank, g->nranks);
                 BFSX_LAUNCHED(st);
                 summed = true;
             }
             td_levels++;
+        } else if (sparse_exchange(g, nf, rank_nf)) {
+            // a small global frontier travels as an id list (4-8 B per id instead of the n/8-byte bitmap
+            // all-gather): every rank sends its ids to every rank, then sets them in the global bitmap
+            const int64_t mine = ws->d_nf;
+            if (int e = grow(ws, ws->sendbuf, ws->send_cap, std::max<int64_t>(mine, 1))) return e;
+            if (int e = grow(ws, ws->recvbuf, ws->recv_cap, std::max<int64_t>(nf, 1))) return e;
+            const uint32_t *ids = ws->qa;
+            if (!ws->d_in_queue) { // the last pull level's record -> local ids
+                BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
+                const int64_t per_block_min = (int64_t)kBS * kCompactWords;
+                const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
+                const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
+                hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, bmf, ws->nwords, wpb, ws->qb,
+                                   ws->d_cursor, ws->nwords * 64);
+                BFSX_LAUNCHED(st);
+                ids = ws->qb;
+            }
+            if (mine > 0) {
+                hipLaunchKernelGGL(k_ids_global, dim3(clamp_grid((mine + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ids,
+                                   (u64)mine, (uint32_t)g->v_lo, ws->sendbuf);
+                BFSX_LAUNCHED(st);
+            }
+            plan_broadcast(P, mine, rank_nf.data(), plan);
+            u64 *rec = nullptr;
+            if (int e = recs.take(&rec)) return e;
+            if (int e = check_live(g, ws, level, "sparse frontier exchange + pull kernel",
+                                   {{"sendbuf", ws->sendbuf}, {"recvbuf", ws->recvbuf}, {"fglob", ws->fglob},
+                                    {"record", rec}, {"vis", ws->vis}, {"parents", ws->par}}))
+                return e;
+            if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
+                                      plan.rcount.data(), plan.rdispl.data(), st))
+                return e;
+            BFSX_HIP_TRY(hipMemsetAsync(ws->fglob, 0, (size_t)ws->nwords * P * sizeof(u64), st));
+            if (plan.recv_total > 0) {
+                hipLaunchKernelGGL(k_ids_to_bitmap, dim3(clamp_grid((plan.recv_total + kBS - 1) / kBS, cap)), dim3(kBS),
+                                   0, st, ws->recvbuf, (u64)plan.recv_total, ws->fglob);
+                BFSX_LAUNCHED(st);
+            }
+            ws->d_in_queue = false;
+            if (int e = launch_bu<false>(g, ws, ws->fglob, rec, ws->par, level)) return e;
+            recs.done(level + 1);
+            bmf = rec;
+            bu_levels++;
         } else {
             if (ws->d_in_queue) { // local queue -> bitmap slice
                 if (was_snapped) { // front holds the visited slice from before the last top-down level
@@ -4189,7 +4261,8 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         examined += h[3];
         visited_local += h[0];
         if (td) std::swap(ws->qa, ws->qb);
-        dmax_local = td ? h[7] : (h[11] == 0 ? (int64_t)opt.hub_degree : -1);
+        dmax_local = td ? h[7] : (h[7] == 0 ? (int64_t)opt.hub_degree : -1);
+        rank_nf.assign(h + 11, h + 11 + P);
         ws->d_dir = dir;
         ws->d_in_queue = td;
         ws->d_nf = h[0];

@@ -139,6 +139,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 queue entry past its tail: the id guard must fail the BFS), "bu_force_spill" = on|off (the
  *                 partitioned pull kernel in a build that spills to scratch), "check_retired" = on|off (the
  *                 partitioned loop fails when a launch or exchange would use a replaced (retired) buffer)
+ *   "sparse_exchange" = auto|on|off (partitioned graphs: a pull level whose global frontier holds fewer than
+ *                 n/128 vertices receives it as every rank's id list instead of the n/8-byte bitmap
+ *                 all-gather (auto, the default); on: every pull level at P > 1; off: never)
  *   "big_degree", "big_cap" = int (partitioned graphs: the ids of degree > big_degree, at most big_cap per
  *                 rank, are all-gathered with their degrees at the first BFS, so every rank knows a source's
  *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS) */

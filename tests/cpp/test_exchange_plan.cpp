@@ -177,12 +177,36 @@ static void slot_case(int P, uint32_t chunk, int64_t slot, std::mt19937_64 &rng)
     }
 }
 
+// The sparse frontier exchange: every rank's id list reaches every rank, in rank order.
+static void broadcast_case(int P, std::mt19937_64 &rng) {
+    std::vector<Rank> R(P);
+    std::vector<u64> counts(P);
+    for (int r = 0; r < P; r++) {
+        counts[r] = rng() % 50;
+        for (u64 i = 0; i < counts[r]; i++) R[r].send.push_back(((u64)r << 40) | i);
+    }
+    for (int r = 0; r < P; r++) {
+        plan_broadcast(P, (int64_t)counts[r], counts.data(), R[r].plan);
+        CHECK(R[r].plan.send_total == (int64_t)counts[r]);
+        R[r].recv.assign((size_t)R[r].plan.recv_total, ~0ull);
+    }
+    run_p2p(P, R);
+    const auto lg = local_group(P, R);
+    for (int q = 0; q < P; q++) {
+        CHECK(lg[q] == R[q].recv);
+        std::vector<u64> want;
+        for (int p = 0; p < P; p++) want.insert(want.end(), R[p].send.begin(), R[p].send.end());
+        CHECK(R[q].recv == want);
+    }
+}
+
 int main() {
     std::mt19937_64 rng(0x5EED);
     for (int P : {1, 2, 3, 4, 8}) {
         for (int t = 0; t < 20; t++) {
             counted_case(P, 64 * (1 + (uint32_t)(rng() % 8)), 500, rng);
             slot_case(P, 64 * (1 + (uint32_t)(rng() % 8)), 1 + (int64_t)(rng() % 40), rng);
+            broadcast_case(P, rng);
         }
         counted_case(P, 64, 0, rng); // every rank sends nothing
     }

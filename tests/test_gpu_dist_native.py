@@ -91,6 +91,30 @@ def test_native_group_random(bfsx, world, direction):
     check(nv, u, v, sources, out)
 
 
+@pytest.mark.parametrize("mode", ["on", "off"])
+@pytest.mark.parametrize("world,direction", [(2, "auto"), (3, "bottomup"), (4, "auto")])
+def test_native_group_sparse_frontier_exchange(bfsx, world, direction, mode):
+    """Option sparse_exchange: a partitioned pull level receives the global frontier as every rank's id list
+    (alltoallv of the per-rank lists, the sizes from the last level close's all-reduce) instead of the bitmap
+    all-gather.  "on" forces it on every pull level after the first level (pull -> pull included: the record
+    is turned into ids), "off" never: bit-exact against the oracle both ways, on random and Kronecker graphs."""
+    rng = np.random.default_rng(900 + world)
+    nv = 7000
+    u = rng.integers(0, nv, 6 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 6 * nv).astype(np.uint32)
+    sources = [0, 3500, 6999]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), sources, direction,
+                    options={"sparse_exchange": mode, "check_retired": "on"})
+    check(nv, u, v, sources, out)
+    assert any(2 in o[3] for o in out)  # pull levels ran
+    scale, seed = 15, 0x5BA5
+    ku, kv = O.kronecker(scale, 16, seed)
+    ksrc = [int(ku[1]), int(ku[2024])]
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, seed=seed), ksrc, direction,
+                    options={"sparse_exchange": mode})
+    check(1 << scale, ku, kv, ksrc, out)
+
+
 @pytest.mark.parametrize("world,direction", [(2, "auto"), (2, "topdown"), (3, "auto"), (4, "bottomup")])
 def test_native_group_no_retired_buffer_referenced(bfsx, world, direction):
     """DESIGN.md 4, event (b): with option check_retired, every launch group and exchange of the partitioned
