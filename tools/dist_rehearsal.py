@@ -99,9 +99,27 @@ def main():
                "wall_ms_max_over_ranks": round(max(x[1] for x in res) * 1e3, 2),
                "validation_errors": res[0][2]["errors"], "validated_entries": res[0][2]["entries"],
                "levels_rank0": res[0][3], "levels_all_ranks": [x[3] for x in res]}
-        # exchange volumes implied by the level records (all ranks): a bottom-up level all-gathers the
-        # n/8-byte frontier bitmap to every rank; a top-down level ships <= 8 B per remote (vertex, parent) pair
-        rec["allgather_bytes_per_bu_level"] = (1 << a.scale) // 8
+        # exchange volumes from the level records (all ranks), per level, bytes received summed over the ranks:
+        #   push level: the (vertex, parent) pairs the ranks shipped (8 B each; `walked` of a push record);
+        #   pull level: the global frontier -- as id lists (8 B per id to every rank) when it holds fewer than
+        #   n/128 vertices (option sparse_exchange=auto, the default), else the n/8-byte bitmap all-gathered
+        #   (each rank receives the P - 1 slices it does not own)
+        n = 1 << a.scale
+        ex = []
+        for li, lv in enumerate(res[0][3]):
+            per = [x[3][li] for x in res]
+            if lv["direction"] == 2:
+                nf = sum(x["frontier_in"] for x in per)
+                sparse = P > 1 and li > 0 and nf * 128 < n
+                b = nf * 8 * (P - 1) if sparse else (n // 8) * (P - 1)
+                ex.append({"level": lv["level"], "kind": "pull", "frontier_in": nf,
+                           "exchange": "id lists" if sparse else "bitmap all-gather", "bytes": b})
+            else:
+                pairs = sum(x["walked"] for x in per)
+                ex.append({"level": lv["level"], "kind": "push", "frontier_in": sum(x["frontier_in"] for x in per),
+                           "exchange": "pairs", "bytes": pairs * 8})
+        rec["exchange"] = ex
+        rec["exchange_bytes_total"] = sum(x["bytes"] for x in ex)
         out["bfs"].append(rec)
         print(json.dumps({k: rec[k] for k in rec if not k.startswith("levels_")}), flush=True)
         assert rec["validation_errors"] == 0
