@@ -781,7 +781,7 @@ struct alignas(128) PersistCtl {
 };
 // host-visible result of one launch (mapped pinned memory, written by workgroup 0)
 struct alignas(64) PersistOut {
-    u64 levels, abort, t0, pad[5];
+    u64 levels, abort, t0, done, pad[4]; // done: set by workgroup 0 once levels / abort / the records are final
     PersistRec rec[kPersistLevels];
 };
 
@@ -882,6 +882,13 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
             }
         }
     }
+}
+
+// K3p's end for the host: every record / count store of workgroup 0 drained and made visible system-wide before
+// the flag (PersistOut lives in mapped pinned host memory).
+__device__ inline void persist_done(PersistOut *out) {
+    __threadfence_system();
+    *reinterpret_cast<volatile u64 *>(&out->done) = 1ull;
 }
 
 // alpha <= 0: no direction switch (direction forced top-down).  q0: the first level's (light) frontier
@@ -1048,6 +1055,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             if (b == 0 && tid == 0) {
                 out->abort = 1;
                 out->levels = (u64)it;
+                persist_done(out);
             }
             return;
         }
@@ -1142,6 +1150,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                 if (b == 0 && tid == 0) {
                     out->abort = 1;
                     out->levels = (u64)it;
+                    persist_done(out);
                 }
                 return;
             }
@@ -1222,6 +1231,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                           (alpha > 0 && (int64_t)mf_new > mu / alpha && (int64_t)mf_new > bu_floor) ||
                           it + 1 >= max_levels;
         __syncthreads();
+        // the host reads the counts as soon as they are final (a mapped flag, no stream synchronise: that cost ~13 us
+        // per launch); the hand-back below is stream-ordered before the next kernel anyway
+        if (stop && b == 0 && tid == 0) persist_done(out);
         if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones
             const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
             for (uint32_t i = tid; i < nb; i += kBS) qfinal[ob + i] = (uint32_t)ld_sc1(sout + 2 * i + 1);
@@ -2903,6 +2915,8 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
     auto *out = reinterpret_cast<PersistOut *>(ws->h_pout);
     out->levels = 0;
     out->abort = 0;
+    out->done = 0;
+    std::atomic_thread_fence(std::memory_order_release);
     const int alpha = opt.direction == BFSX_DIR_AUTO ? std::max(opt.alpha, 1) : 0;
     auto *ctl = reinterpret_cast<PersistCtl *>(ws->persist_ctl);
     auto *dout = reinterpret_cast<PersistOut *>(ws->d_pout);
@@ -2927,7 +2941,19 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    // spin on workgroup 0's flag; poll the stream now and then so a faulted launch surfaces as an error
+    const volatile u64 *done = &out->done;
+    for (uint64_t spin = 1; *done == 0; spin++) {
+        if ((spin & 0xFFFF) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(BFSX_E_HIP, std::string("persistent top-down: ") + hipGetErrorString(e));
+            if (e == hipSuccess && *done == 0) {
+                ws->persist_reset = true;
+                return fail(BFSX_E_HIP, "persistent top-down: the launch ended without its done flag");
+            }
+        }
+    }
     std::atomic_thread_fence(std::memory_order_acquire);
     if (out->abort) {
         ws->persist_reset = true;
