@@ -559,14 +559,13 @@ def launch_ranks(args):
     process, `python -m torch.distributed.run --nproc-per-node N ... bench.py <the same arguments>`, before
     this process touches HIP or torch, relay the child's single JSON line to stdout and return its exit
     code.  Everything else the child prints goes to stderr."""
-    import socket
     import subprocess
 
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    # the c10d rendezvous binds port 0 itself (a port probed here and handed over could be taken in between:
+    # ADVICE r3); --local-addr keeps MASTER_ADDR at 127.0.0.1 (the container hostname may not resolve)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
+           os.path.abspath(__file__)] + sys.argv[1:]
     print(f"[bench] --gpus {args.gpus}: launching {' '.join(cmd)}", file=sys.stderr, flush=True)
     r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]

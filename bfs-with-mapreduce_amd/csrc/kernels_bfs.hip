@@ -839,14 +839,21 @@ __device__ __forceinline__ void persist_step(uint32_t x0, uint32_t x_end, const 
         r0[k] = valid[k] ? (int64_t)row_off[v[k]] : 0;
         r1[k] = valid[k] ? (int64_t)row_off[v[k] + 1] : 0;
     }
+    // every item's claim in flight before any result is used (a ballot per item would wait out one atomic
+    // round trip per item in turn)
+    u64 old[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
         const u64 bit = 1ull << (v[k] & 63u);
-        bool win = false;
+        old[k] = bit;
         if (!(wv[k] & bit)) {
             attempts++;
-            win = !(atomicOr(vis + (v[k] >> 6), bit) & bit);
+            old[k] = atomicOr(vis + (v[k] >> 6), bit);
         }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        const bool win = !(old[k] & (1ull << (v[k] & 63u)));
         const u64 dg = win ? (u64)(r1[k] - r0[k]) : 0ull;
         bool heavy = false;
         if (win) {
