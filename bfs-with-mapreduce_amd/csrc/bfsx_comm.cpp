@@ -44,8 +44,10 @@ class RcclComm final : public Comm {
         return BFSX_OK;
     }
     int alltoall1(const int64_t *d_send, int64_t *d_recv, hipStream_t st) override {
+        if (nranks < 2) return BFSX_OK; // the own entry is not exchanged (Comm::alltoall1)
         BFSX_NCCL_TRY(ncclGroupStart());
         for (int p = 0; p < nranks; p++) {
+            if (p == rank) continue;
             BFSX_NCCL_TRY(ncclSend(d_send + p, 1, ncclInt64, p, comm, st));
             BFSX_NCCL_TRY(ncclRecv(d_recv + p, 1, ncclInt64, p, comm, st));
         }
@@ -56,6 +58,7 @@ class RcclComm final : public Comm {
                   const int64_t *rcount, const int64_t *rdispl, hipStream_t st) override {
         std::vector<P2pOp> ops;
         alltoallv_ops(nranks, scount, sdispl, rcount, rdispl, ops);
+        if (ops.empty()) return BFSX_OK;
         BFSX_NCCL_TRY(ncclGroupStart());
         for (const P2pOp &o : ops) {
             if (o.send) BFSX_NCCL_TRY(ncclSend(d_send + o.offset, (size_t)o.count, ncclUint64, o.peer, comm, st));

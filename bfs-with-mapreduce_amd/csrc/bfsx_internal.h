@@ -69,7 +69,8 @@ struct Comm {
     int rank = 0, nranks = 1;
     virtual ~Comm() = default;
     virtual int allreduce_sum(int64_t *d_buf, int n, hipStream_t st) = 0;              // in place
-    virtual int alltoall1(const int64_t *d_send, int64_t *d_recv, hipStream_t st) = 0; // one value per rank
+    // one value per rank; d_recv[rank] (the value a rank sends itself) may be left unwritten
+    virtual int alltoall1(const int64_t *d_send, int64_t *d_recv, hipStream_t st) = 0;
     virtual int alltoallv(const unsigned long long *d_send, const int64_t *scount, const int64_t *sdispl, unsigned long long *d_recv,
                           const int64_t *rcount, const int64_t *rdispl, hipStream_t st) = 0; // host counts
     virtual int allgather(const unsigned long long *d_in, int64_t n, unsigned long long *d_out, hipStream_t st) = 0;

@@ -47,12 +47,16 @@ inline void plan_counted(int P, const U *send_counts, const U *recv_counts, Exch
 
 // Fixed slots of (slot + 1) words per peer: word 0 = the pair count, then up to `slot` pairs.  The
 // receiver's claim kernel reads P * slot candidate entries (entry i -> peer i / slot, pair i % slot).
-inline void plan_slots(int P, int64_t slot, ExchangePlan &pl) {
+// self: this rank.  Its own slot is never exchanged -- the push kernels claim their own vertices directly, so
+// it is always empty -- and the claim kernel skips it (at P = 1 the level exchanges nothing).  The buffers
+// keep the slot's space, so every peer's slot sits at the same offset on both sides.
+inline void plan_slots(int P, int64_t slot, ExchangePlan &pl, int self = -1) {
     pl.scount.assign(P, slot + 1);
     pl.rcount.assign(P, slot + 1);
     pl.sdispl.assign(P, 0);
     pl.rdispl.assign(P, 0);
     for (int p = 0; p < P; p++) pl.sdispl[p] = pl.rdispl[p] = (int64_t)p * (slot + 1);
+    if (self >= 0 && self < P) pl.scount[self] = pl.rcount[self] = 0;
     pl.send_total = pl.recv_total = (int64_t)P * (slot + 1);
 }
 
@@ -75,11 +79,13 @@ inline void plan_broadcast(int P, int64_t mine, const U *counts, ExchangePlan &p
     pl.recv_total = ro;
 }
 
-// Word offset of candidate entry i of a received slot exchange, or -1 when entry i is past its peer's count.
+// Word offset of candidate entry i of a received slot exchange, or -1 when entry i is past its peer's count
+// or in the receiver's own (unexchanged) slot.
 template <class U>
-inline int64_t slot_entry(const U *recv, int64_t i, int64_t slot) {
+inline int64_t slot_entry(const U *recv, int64_t i, int64_t slot, int self = -1) {
     const int64_t p = i / slot, k = i - p * slot;
     const int64_t base = p * (slot + 1);
+    if (p == self) return -1;
     return k < (int64_t)recv[base] ? base + 1 + k : -1;
 }
 

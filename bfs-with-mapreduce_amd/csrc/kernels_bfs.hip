@@ -1309,10 +1309,10 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
         uint32_t vl = 0;
         bool have = i < npairs;
         u64 at = i;
-        if (have && slot) {
+        if (have && slot) { // the own slot is not exchanged (plan_slots): skipped
             const u64 p = i / slot, k = i - p * slot;
             const u64 base = p * (slot + 1);
-            have = k < pairs[base];
+            have = p != (u64)rank && k < pairs[base];
             at = base + 1 + k;
         }
         if (have) {
@@ -1476,6 +1476,11 @@ __device__ inline uint32_t probe_hub(const u64 *__restrict__ front, const u64 *_
 // overlap the probes, stage A2 and phase B instead of opening the next round (one dependent memory
 // latency fewer per round; a half-group of dense candidates runs up to 8 rounds).
 constexpr uint32_t kPrefIds = 1u << 16; // LDS frontier prefix: 8 KiB per workgroup
+// A 64-word group's candidates are listed in kBuParts parts (kBuCand LDS slots per wave).  Round 4 measured 4 parts
+// (22.8 KiB of LDS) at 5 and 6 waves per SIMD and 8 parts at 6: the pull kernel got 3-9% slower each time (fewer
+// candidates per round), so 2 parts (31 KiB, 5 waves per SIMD) stay.
+constexpr int kBuParts = 2;
+constexpr uint32_t kBuCand = 64u * 64u / (uint32_t)kBuParts;
 // The ids whose frontier bits the pull kernel reads from LDS: the first `ids` ids of each of `nseg` id
 // ranges of 2^shift ids (one range on one device, shift >= 32 = the whole id space; a partition's
 // ranks' ranges).  ids = 0: off.
@@ -1506,7 +1511,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
     __shared__ u64 s_nx[kWaves][64];
     // phase B's rows; the hub sweep (kHubOnly) carries them over rounds until a full 64-lane batch is ready
     __shared__ uint32_t s_miss[kWaves][(64 * kU) + (kHubOnly ? 64 : 0)];
-    __shared__ uint16_t s_cand[kWaves][2048]; // candidate offsets (v - group base) of one half-group
+    __shared__ uint16_t s_cand[kWaves][kBuCand]; // candidate offsets (v - group base) of one part of the group
     // the frontier bits of the first pf.ids ids of every id range (the highest-degree vertices of a
     // relabelled graph, where most probes land) copied to LDS once per workgroup; pf.ids = 0: off
     __shared__ uint32_t s_pref[kPrefIds / 32];
@@ -1549,13 +1554,13 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
         s_nx[wave][lane] = 0ull;
         __builtin_amdgcn_wave_barrier();
         const uint32_t vbase = (uint32_t)(w0 * 64);
-        // the group's candidates, one half (32 words, <= 2048 vertices) at a time: each word's lane
-        // writes the offsets of its unvisited bits at its rank, then rounds of (64 * kU) candidates
-        const uint32_t half = __shfl(incl, 31); // candidates in words 0..31
-        for (int h = 0; h < 2; h++) {
-            const uint32_t hb = h ? half : 0u, he = h ? total : half;
+        // the group's candidates, one part (64 / kBuParts words, <= kBuCand vertices) at a time: each word's
+        // lane writes the offsets of its unvisited bits at its rank, then rounds of (64 * kU) candidates
+        for (int h = 0; h < kBuParts; h++) {
+            constexpr int kWp = 64 / kBuParts; // words per part
+            const uint32_t hb = h ? __shfl(incl, h * kWp - 1) : 0u, he = __shfl(incl, (h + 1) * kWp - 1);
             if (hb == he) continue; // wave-uniform
-            if ((lane >> 5) == (unsigned)h) {
+            if ((int)(lane / kWp) == h) {
                 u64 bits = unv;
                 uint32_t idx = excl - hb;
                 while (bits) {
@@ -1589,7 +1594,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                     for (int k = 0; k < kU; k++) {
                         x[k] = xn[k];
                         const uint32_t at = t1 - hb + (uint32_t)k * 64 + lane; // past the list: unused (masked below)
-                        vn[k] = vbase + s_cand[wave][at < 2048u ? at : 0u];
+                        vn[k] = vbase + s_cand[wave][at < kBuCand ? at : 0u];
                     }
                 } else {
 #pragma unroll
@@ -4088,6 +4093,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     const u64 *bmf = ws->front;
     RecLog recs(g, ws);
     std::vector<int64_t> rank_nf; // every rank's frontier size after the last level close (all-reduced)
+    int64_t nf_core = -1;         // after a pull level: its local discoveries below leaf_lo (-1: unknown)
     ExchangePlan plan;
     std::vector<u64> hc(2 * kMaxRanks);
     for (;;) {
@@ -4109,15 +4115,23 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         bool summed = false; // the level's last kernel already closed the level (k_claim_remote)
         const bool was_snapped = snapped;
         snapped = false;
+        int64_t nq = ws->d_nf; // the push queue's length
         if (td) {
             if (!ws->d_in_queue) { // local bitmap slice -> queue
+                // leaf skip (as on one device): after a pull level the discoveries at local ids >= leaf_lo have
+                // one adjacency entry, their parent, and sweep nothing; the queue holds the nf_core others (the
+                // pull kernel counted them)
+                const bool skip = opt.leaf_skip && nf_core >= 0 && ws->leaf_lo < g->nv;
+                const int64_t lim = skip ? ws->leaf_lo : ws->nwords * 64;
+                const int64_t cw = (lim + 63) / 64;
                 BFSX_HIP_TRY(hipMemsetAsync(ws->d_cursor, 0, sizeof(u64), st));
                 const int64_t per_block_min = (int64_t)kBS * kCompactWords;
-                const unsigned gb = clamp_grid((ws->nwords + per_block_min - 1) / per_block_min, 256);
-                const int64_t wpb = ((ws->nwords + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
-                hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, bmf, ws->nwords, wpb, ws->qa,
-                                   ws->d_cursor, ws->nwords * 64);
+                const unsigned gb = clamp_grid(std::max<int64_t>((cw + per_block_min - 1) / per_block_min, 1), 256);
+                const int64_t wpb = ((cw + gb - 1) / gb + per_block_min - 1) / per_block_min * per_block_min;
+                hipLaunchKernelGGL(k_bitmap_to_queue, dim3(gb), dim3(kBS), 0, st, bmf, cw, wpb, ws->qa,
+                                   ws->d_cursor, lim);
                 BFSX_LAUNCHED(st);
+                if (skip) nq = nf_core;
                 ws->d_in_queue = true;
             }
             // a wide top-down level may hand over to bottom-up: snapshot the visited slice (see bfs_run)
@@ -4156,7 +4170,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 pt.slot_cap = (u64)slot;
                 pt.slot_cursor = dcursor;
                 pt.slot_arrive = dcount;
-                plan_slots(P, slot, plan);
+                plan_slots(P, slot, plan, g->rank); // the own slot stays empty and is not exchanged
                 ro = P * slot; // candidate entries the claim kernel reads
             }
             if (int e = check_live(g, ws, level, "push kernels",
@@ -4164,7 +4178,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                                     {"state", ws->st}, {"remote", pt.remote}, {"slot_out", pt.slot_out},
                                     {"counters", ws->d_dist_ctr}, {"front", ws->front}}))
                 return e;
-            if (int e = launch_td<true>(g, ws, ws->d_nf, ws->d_mf, dmax_local, level, pt)) return e;
+            if (int e = launch_td<true>(g, ws, nq, ws->d_mf, dmax_local, level, pt)) return e;
             if (!slot) {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, P, dcount);
@@ -4176,6 +4190,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
                     return e;
                 if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
+                hc[P + g->rank] = 0; // alltoall1 does not exchange the own entry (no pairs route to it)
                 plan_counted(P, hc.data(), hc.data() + P, plan);
                 ro = plan.recv_total;
                 if (int e = grow(ws, ws->recvbuf, ws->recv_cap, std::max<int64_t>(ro, 1))) return e;
@@ -4295,6 +4310,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         visited_local += h[0];
         if (td) std::swap(ws->qa, ws->qb);
         dmax_local = td ? h[7] : (h[7] == 0 ? (int64_t)opt.hub_degree : -1);
+        nf_core = td ? -1 : h[1]; // a pull level's local discoveries below leaf_lo (k_bu counts them in m_f)
         rank_nf.assign(h + 11, h + 11 + P);
         ws->d_dir = dir;
         ws->d_in_queue = td;

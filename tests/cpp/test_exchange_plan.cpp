@@ -68,7 +68,7 @@ static void run_p2p(int P, std::vector<Rank> &R) {
 static std::vector<std::vector<u64>> local_group(int P, const std::vector<Rank> &R) {
     std::vector<std::vector<u64>> out(P);
     for (int q = 0; q < P; q++) {
-        out[q].assign(R[q].recv.size(), 0);
+        out[q].assign(R[q].recv.size(), ~0ull); // words no block lands on stay as the receive buffer had them
         for (int p = 0; p < P; p++)
             for (int64_t i = 0; i < R[q].plan.rcount[p]; i++)
                 out[q][R[q].plan.rdispl[p] + i] = R[p].send[R[p].plan.sdispl[q] + i];
@@ -149,7 +149,8 @@ static void slot_case(int P, uint32_t chunk, int64_t slot, std::mt19937_64 &rng)
             if (P == 1) continue;
             R[r].remote.push_back(((u64)v << 32) | (u64)i);
         }
-        plan_slots(P, slot, R[r].plan);
+        plan_slots(P, slot, R[r].plan, r);
+        CHECK(R[r].plan.scount[r] == 0 && R[r].plan.rcount[r] == 0); // the own slot is not exchanged
         // k_bucket_slots + k_slot_headers
         R[r].send.assign((size_t)R[r].plan.send_total, 0);
         std::vector<u64> cur(P, 0);
@@ -167,7 +168,7 @@ static void slot_case(int P, uint32_t chunk, int64_t slot, std::mt19937_64 &rng)
         // k_claim_remote's entry mapping over P * slot candidates
         std::multiset<u64> got, want;
         for (int64_t i = 0; i < (int64_t)P * slot; i++) {
-            const int64_t at = slot_entry(R[q].recv.data(), i, slot);
+            const int64_t at = slot_entry(R[q].recv.data(), i, slot, q);
             if (at >= 0) got.insert(R[q].recv[at]);
         }
         for (int p = 0; p < P; p++)
