@@ -2823,8 +2823,12 @@ int64_t bu_floor(const bfsx_graph *g, const BfsWorkspace *ws) {
 }
 
 // K3p geometry: at most one workgroup per CU and at most kBS (every workgroup reads all records).
+// auto: three workgroups per four CUs.  Every workgroup polls every record at each level's barrier, and the
+// slowest of G dependent chains sets the level: on the largeG stand-in 160-192 workgroups give 10.6-10.7 us per
+// level against 11.1 at 256 (96: 10.8, 32: 12.1), and scale 26 is level or better
+// (profiles/r04y_k3p_grid_largeg.txt, profiles/r04y_k3p_grid_scale26_ab.txt).
 int persist_blocks(const bfsx_ctx *ctx) {
-    const int want = ctx->opt.persist_blocks > 0 ? ctx->opt.persist_blocks : ctx->num_cus;
+    const int want = ctx->opt.persist_blocks > 0 ? ctx->opt.persist_blocks : std::max(1, ctx->num_cus * 3 / 4);
     return std::max(1, std::min({want, ctx->num_cus, kBS}));
 }
 

@@ -216,7 +216,7 @@ def test_row_order_option(ctx, order, relabel):
 def test_persistent_topdown_matches_per_level_kernels(ctx, case, blocks):
     """K3p (narrow frontiers, many levels per launch) against the per-level kernels and the oracle:
     identical distances, level counts, per-level frontier sizes, monotone level times; two sources per
-    graph (the barrier counters carry over between launches).  blocks: K3p workgroups (auto = one per CU;
+    graph (the barrier counters carry over between launches).  blocks: K3p workgroups (auto = three per four CUs;
     3 = uneven slices, several steps per slice).  lollipop: a path into a 20000-leaf star, whose hub
     must hand back to the per-level kernels (a slice could overflow its output segment)."""
     if case == "path":
@@ -317,7 +317,7 @@ def test_persist_blocks_changed_between_runs(ctx):
     """persist_blocks raised after a graph's first K3p launch: the launch keeps the grid it was set up
     with, and the entry bound (every slice fits its output segment) is checked against THAT grid."""
     # root 0 -> 1000 children -> 40 leaves each: the second frontier (1000 vertices of degree 41) fits a
-    # 256-workgroup grid's segments (4 x 41 entries) but not a 2-workgroup grid's (500 x 40 discoveries)
+    # 192-workgroup (auto) grid's segments (6 x 41 entries) but not a 2-workgroup grid's (500 x 40 discoveries)
     kids, fan = 1000, 40
     nv = 1 + kids + kids * fan
     child = np.arange(1, kids + 1)

@@ -28,12 +28,19 @@ def standin(side=1000, m=7_586_063, radius=2, seed=2026):  # the generator of te
 
 nv, u, v = standin()
 ctx = bfsx.Context(0)
-with ctx.from_edges(nv, u, v) as g:
+# FRESH=1: a new graph per setting (K3p keeps the grid of a graph's first launch, so a persist_blocks sweep
+# needs one graph per value)
+fresh = os.environ.get("FRESH") == "1"
+g = ctx.from_edges(nv, u, v)
+with g:
     ref = None
     for arg in sys.argv[1:] or ["persist_blocks=auto"]:
         k, vals = arg.split("=", 1)
         for val in vals.split(","):
             ctx.set_option(k, val)
+            if fresh:
+                g.free()
+                g = ctx.from_edges(nv, u, v)
             ts = []
             for _ in range(4):
                 d, _, st = g.bfs(0, want_parent=False)
