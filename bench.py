@@ -148,10 +148,12 @@ def common_fields(args, world, value, wall, nv, m, nnz, nroots, parallelism):
     }
 
 
-def measured_traffic(kernel="k_bu"):
+def measured_traffic(kernel="k_bu", nwords=None):
     """Per-launch HBM bytes of `kernel` from the newest committed PMC summary (profiles/<tag>_hbm.json,
     written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes),
-    used only while kernels_bfs.hip still hashes to the source it was measured on."""
+    used only while kernels_bfs.hip still hashes to the source it was measured on, and only for the graph
+    size it was measured on (nwords: bitmap words of the bench's graph; a scale-26 profile says nothing
+    about a scale-30 launch)."""
     import glob
     import hashlib
     src = os.path.join(PKG, "csrc", "kernels_bfs.hip")
@@ -162,7 +164,7 @@ def measured_traffic(kernel="k_bu"):
         except (OSError, ValueError):
             continue
         names = [n for n in rec.get("kernels", {}) if n == kernel or n.startswith(kernel + "<")]
-        if rec.get("kernels_bfs_sha") == sha and names:
+        if rec.get("kernels_bfs_sha") == sha and names and (nwords is None or rec.get("nwords") == nwords):
             # the instantiation with the most launches (the hybrid levels' hub sweep is a second one)
             k = max((rec["kernels"][n] for n in names), key=lambda x: x.get("launches", 0))
             # per-access-class correction when the summary has it (round 3: profiles/r03k_fetch_calibration.json),
@@ -178,7 +180,7 @@ def measured_traffic(kernel="k_bu"):
                 out["traffic_GBs"] = round(tb / (k["avg_ms_trace"] * 1e-3) / 1e9, 1)
                 out["traffic_frac"] = round(out["traffic_GBs"] / PEAK_HBM_GBS, 4)
             return out
-    return {"traffic": None, "traffic_source": "no PMC summary for this kernel source"}
+    return {"traffic": None, "traffic_source": "no PMC summary for this kernel source and graph size"}
 
 
 class LevelAccount:
@@ -204,7 +206,7 @@ class LevelAccount:
     def roofline(self, note):
         n = self.bu_launches
         ach = (self.bu_bytes / n) / ((self.bu_ms / n) * 1e-3) / 1e9 if n else 0.0
-        tr = measured_traffic()
+        tr = measured_traffic(nwords=self.nwords)
         return {
             "bound": "hbm",
             "kernel": "k_bu (bottom-up pull)",

@@ -75,7 +75,7 @@ def main():
         sha = open(os.path.join(d, "src_sha")).read().split()[0][:16]
     except OSError:
         sha = src_hash()
-    res = {"tag": tag, "kernels_bfs_sha": sha, "fetch_correction": corr,
+    res = {"tag": tag, "kernels_bfs_sha": sha, "nwords": nwords, "fetch_correction": corr,
            "fetch_correction_basis": "k_finalize reads exactly 8*nwords B (8 B/lane coalesced)"
            if "k_finalize" in fetch else "guide default (x2 for wide streaming reads)",
            "kernels": {}}
