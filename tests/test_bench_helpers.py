@@ -22,7 +22,7 @@ def test_bottom_up_level_bytes(bench):
     nwords = 64
     # single device: a discovery stores its 4-B parent (the level record gives the distance)
     assert bench.level_bytes(ls, nwords) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 4 * 600
-    # partitioned loop: the packed 8-B state
+    # a packed 8-B state store per discovery (round 3's pull levels)
     assert bench.level_bytes(ls, nwords, found_bytes=8) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 8 * 600
 
 
@@ -97,6 +97,11 @@ def test_measured_traffic_requires_matching_source(bench, tmp_path, monkeypatch)
     monkeypatch.setattr(bench, "PKG", os.path.join(ROOT, "bfs-with-mapreduce_amd"))
     out = bench.measured_traffic()
     assert out["traffic"] == 1200.0 and out["traffic_GBs"] == 4800.0
+    # and only for the graph size it was measured on (a scale-26 profile says nothing about scale 30)
+    rec["nwords"] = 1 << 20
+    (prof / "zz_hbm.json").write_text(json.dumps(rec))
+    assert bench.measured_traffic(nwords=1 << 20)["traffic"] == 1200.0
+    assert bench.measured_traffic(nwords=1 << 24)["traffic"] is None
     rec["kernels_bfs_sha"] = "0" * 16
     (prof / "zz_hbm.json").write_text(json.dumps(rec))
     assert bench.measured_traffic()["traffic"] is None
