@@ -1487,8 +1487,8 @@ constexpr uint32_t kBuCand = 64u * 64u / (uint32_t)kBuParts;
 struct PrefixSpec {
     uint32_t ids, nseg, shift, pad;
 };
-// A pull level's discovery: single device, the 4-B parent only (the level's record bitmap gives the distance,
-// BfsWorkspace::par); partitioned (par_out == null), the packed state.
+// A pull level's discovery: the 4-B parent only (the level's record bitmap gives the distance, BfsWorkspace::par;
+// one device and the partitioned loop alike); par_out == null: the packed state.
 __device__ __forceinline__ void settle_state(u64 *__restrict__ stt, uint32_t *__restrict__ par_out, uint32_t v,
                                              uint32_t parent, int32_t nd) {
     if (par_out) par_out[v] = parent;
@@ -2149,6 +2149,30 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, con
             const uint32_t p = (uint32_t)(s >> 32);
             const uint32_t po = (!kRelabel || p == 0xFFFFFFFFu) ? p : inv[p];
             out[o] = ((u64)po << 32) | (uint32_t)s;
+        }
+    }
+}
+
+// The same in ORIGINAL id order (a relabelled graph, round 4): thread o reads perm[o] and writes out[o], so the
+// writes are whole lines.  The reads stay near-sequential: the relabel sorts by degree with ties in original
+// order, so the vertices of one degree class keep their original order in the internal ids -- consecutive
+// original ids read K advancing streams (one per degree class present), whose lines L2 holds.  Every entry is
+// written (isolated ones as unreached, except the source), so no prefill is needed.  The scatter form above
+// writes one 8-B word per 64-B line (consecutive internal ids of a class are original ids several apart).
+__global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
+                                                       RecSet rs, const uint32_t *__restrict__ perm,
+                                                       const uint32_t *__restrict__ inv, int64_t n,
+                                                       const u64 *__restrict__ dead, int64_t src,
+                                                       u64 *__restrict__ out, int32_t *__restrict__ dist_only) {
+    for (int64_t o = (int64_t)blockIdx.x * kBS + threadIdx.x; o < n; o += (int64_t)gridDim.x * kBS) {
+        const int64_t i = (int64_t)perm[o];
+        u64 s = kUnreached;
+        if (!((dead[i >> 6] >> (i & 63)) & 1ull) || i == src) s = rec_state(stt, par, rs, i);
+        if (dist_only) {
+            dist_only[o] = (int32_t)(uint32_t)s;
+        } else {
+            const uint32_t p = (uint32_t)(s >> 32);
+            out[o] = ((u64)(p == 0xFFFFFFFFu ? p : inv[p]) << 32) | (uint32_t)s;
         }
     }
 }
@@ -3509,7 +3533,9 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     int32_t *d_dist_only = packed ? nullptr : reinterpret_cast<int32_t *>(ws->out64);
     const dim3 grid(clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192));
     const int mode = packed ? 1 : 2;
-    if (ws->out_mode != mode) { // every entry unreached once; isolated vertices keep it from then on
+    // a relabelled graph unpacks in original id order and writes every entry (k_unpack_gather): no prefill
+    const bool gather = g->d_perm != nullptr && g->d_inv != nullptr;
+    if (!gather && ws->out_mode != mode) { // every entry unreached once; isolated vertices keep it from then on
         if (packed) {
             hipLaunchKernelGGL(k_fill64, grid, dim3(kBS), 0, st, ws->out64, (int64_t)nv, kUnreached);
         } else {
@@ -3522,15 +3548,19 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     }
     // the source's local row (a partition's non-owning ranks: none)
     const int64_t src = (g->last_source >= g->v_lo && g->last_source < g->v_lo + g->nv) ? g->last_source - g->v_lo : -1;
-    bool src_dead = false; // an isolated source's entry must be reset by the next unpack
-    if (src >= 0) {
+    bool src_dead = false; // an isolated source's entry must be reset by the next (scatter-form) unpack
+    if (src >= 0 && !gather) {
         u64 dw = 0;
         BFSX_HIP_TRY(hipMemcpyAsync(&dw, ws->dead + (src >> 6), sizeof(dw), hipMemcpyDeviceToHost, st));
         BFSX_HIP_TRY(hipStreamSynchronize(st));
         src_dead = (dw >> (src & 63)) & 1ull;
     }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack0, st));
-    if (g->d_inv)
+    if (gather) {
+        hipLaunchKernelGGL(k_unpack_gather, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_perm, g->d_inv,
+                           (int64_t)nv, ws->dead, src, ws->out64, d_dist_only);
+        ws->out_mode = 0; // every entry written: a later scatter-mode unpack must prefill again
+    } else if (g->d_inv)
         hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo, (int64_t)nv,
                            ws->dead, src, ws->out_dirty, ws->out64, d_dist_only);
     else
