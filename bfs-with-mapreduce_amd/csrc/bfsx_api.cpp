@@ -289,6 +289,12 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "persist must be on|off");
         return BFSX_OK;
     }
+    if (k == "push_log") {
+        if (v == "on") ctx->opt.push_log = true;
+        else if (v == "off") ctx->opt.push_log = false;
+        else return fail(BFSX_E_ARG, "push_log must be on|off");
+        return BFSX_OK;
+    }
     if (k == "persist_blocks") {
         if (v == "auto") {
             ctx->opt.persist_blocks = 0;

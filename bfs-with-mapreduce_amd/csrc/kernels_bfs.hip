@@ -103,7 +103,19 @@ struct BfsWorkspace {
     std::vector<u64 *> prec;            // record pool (grown on demand, kept across BFS runs)
     std::vector<int32_t> prec_nd;       // distance of record k's vertices (its level + 1), last BFS
     int n_prec = 0;                     // records of the last BFS
-    bool resolved = true;               // st holds every reached vertex's state (no record pending)
+    bool resolved = true;               // st holds every reached vertex's state (no record or log pending)
+    // Push log (single device, round 4): the winners of a per-level push level (k_td / k_td_hubs, not K3p) are
+    // written as vertex | parent << 32 at their next-frontier queue positions -- coalesced through the LDS
+    // queue -- instead of one scattered 8-B state store each.  Level k's entries are plog[log_end[k-1],
+    // log_end[k]) with distance log_nd[k]; bfs_resolve / the unpack scatter them into st (apply_logs), outside
+    // the timed region like the pull records.
+    u64 *plog = nullptr;                // nv entries (a vertex is discovered once)
+    int64_t log_n = 0;                  // entries of the last BFS
+    std::vector<int64_t> log_end;
+    std::vector<int32_t> log_nd;
+    bool logs_pending = false;          // entries not yet scattered into st
+    int64_t *d_log_meta = nullptr;      // device copy of log_end + log_nd for k_resolve_log
+    int64_t log_meta_cap = 0;
     uint32_t *off32 = nullptr;          // uint32 copy of the row offsets (nnz < 2^32), else null
     u64 *vis = nullptr, *front = nullptr, *next = nullptr;
     u64 *dead = nullptr;                // isolated vertices + padding (initial visited bitmap)
@@ -371,6 +383,16 @@ struct BlockQueueT {
 using BlockQueue = BlockQueueT<kQCap>;
 // the partitioned push kernels also hold a remote-pair queue: half-size queues keep 4 workgroups per CU
 using DistQueue = BlockQueueT<kQCap / 2>;
+// Single-device push kernels: winners are queued with their parent (vertex | parent << 32, same LDS bytes as
+// BlockQueue); a flush writes the next frontier's ids and, with a push log, the pairs at the same positions.
+template <int kCapT>
+struct LogQueueT {
+    static constexpr uint32_t kCap = kCapT;
+    u64 buf[kCapT];
+    uint32_t n;
+    uint32_t gbase;
+};
+using LogQueue = LogQueueT<kQCap / 2>;
 
 // All 64 lanes of every wave call this (wave-uniform control flow).
 template <class Q>
@@ -402,6 +424,43 @@ __device__ inline void bq_flush(Q &q, uint32_t *__restrict__ qout, u64 *qtail) {
 template <class Q>
 __device__ inline void bq_init(Q &q) {
     if (threadIdx.x == 0) q.n = 0;
+}
+
+// The push kernels' queue calls for either queue type (the id-only queue ignores the parent and the log).
+template <int C>
+__device__ inline void q_push(BlockQueueT<C> &q, bool win, uint32_t v, uint32_t) {
+    bq_push(q, win, v);
+}
+template <int C>
+__device__ inline void q_push(LogQueueT<C> &q, bool win, uint32_t v, uint32_t parent) {
+    const u64 mask = __ballot(win);
+    if (mask == 0) return;
+    const unsigned lane = lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(&q.n, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (win) q.buf[base + __popcll(mask & ((1ull << lane) - 1ull))] = (u64)v | ((u64)parent << 32);
+}
+template <int C>
+__device__ inline void q_flush(BlockQueueT<C> &q, uint32_t *__restrict__ qout, u64 *, u64 *qtail) {
+    bq_flush(q, qout, qtail);
+}
+template <int C>
+__device__ inline void q_flush(LogQueueT<C> &q, uint32_t *__restrict__ qout, u64 *__restrict__ plog, u64 *qtail) {
+    const uint32_t n = q.n;
+    if (n == 0) return;
+    if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(qtail, (u64)n);
+    __syncthreads();
+    const uint32_t gb = q.gbase;
+    for (uint32_t i = threadIdx.x; i < n; i += kBS) {
+        const u64 e = q.buf[i];
+        qout[gb + i] = (uint32_t)e;
+        if (plog) plog[gb + i] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) q.n = 0;
+    __syncthreads();
 }
 
 // ---- K3: top-down push, degree-binned -----------------------------------------------------------
@@ -553,7 +612,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
                                       uint32_t *__restrict__ par, int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
-                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh) {
+                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh, u64 *__restrict__ plog) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -584,8 +643,10 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
             }
             if (valid[k] && !send && claim(vl, vis, attempts)) {
                 win = true;
-                stt[vl] = pack_state(pu[k], nd);
+                // the push log (single device) or the hybrid level's parent array + record carry the result;
+                // else the packed state
                 if (par) par[vl] = pu[k];
+                else if (!plog) stt[vl] = pack_state(pu[k], nd);
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
                 acc_mf += dg;
                 acc_dmax = dg > acc_dmax ? dg : acc_dmax;
@@ -594,11 +655,11 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                     acc_nh += 1;
                 }
             }
-            bq_push(q, win, vl);
+            q_push(q, win, vl, pu[k]);
             if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
         }
         __syncthreads();
-        if (q.n > Q::kCap - (uint32_t)(kBS * kItems)) bq_flush(q, qout, qtail);
+        if (q.n > Q::kCap - (uint32_t)(kBS * kItems)) q_flush(q, qout, plog, qtail);
         if (kDist && rq->n > (uint32_t)(kRCap - kBS * kItems)) rq_flush(*rq, pt);
     }
 }
@@ -609,14 +670,14 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
                                             uint32_t *__restrict__ par, LevelSlot *ring, int level, uint32_t hub_deg,
                                             uint32_t *__restrict__ hubs, Part pt, int gsz, HubSet hs,
-                                            HubSet skip, Published *pub, u64 seq) {
+                                            HubSet skip, Published *pub, u64 seq, u64 *__restrict__ plog) {
     LevelSlot *cn = ring + (level + 1) % 3;
     zero_slot(ring, level);
     __shared__ uint32_t s_scan[kBS + 1];
     __shared__ int64_t s_beg[kBS];
     __shared__ uint32_t s_u[kBS];
     __shared__ uint32_t s_wsum[kWaves];
-    __shared__ typename std::conditional<kDist, DistQueue, BlockQueue>::type q;
+    __shared__ typename std::conditional<kDist, DistQueue, LogQueue>::type q;
     __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
@@ -666,10 +727,10 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
         }
         __syncthreads();
         sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, par, nd, q, qout, &cn->qtail, pt, rq,
-                              acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh);
+                              acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog);
         __syncthreads();
     }
-    bq_flush(q, qout, &cn->qtail);
+    q_flush(q, qout, plog, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
     // top-down: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
@@ -682,13 +743,13 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  u64 *vis, u64 *__restrict__ stt, uint32_t *__restrict__ par,
                                                  LevelSlot *ring, int level,
-                                                 Part pt, HubSet hs, Published *pub, u64 seq) {
+                                                 Part pt, HubSet hs, Published *pub, u64 seq, u64 *__restrict__ plog) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ u64 s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
     __shared__ u64 s_tsum[kBS];
-    __shared__ typename std::conditional<kDist, DistQueue, BlockQueue>::type q;
+    __shared__ typename std::conditional<kDist, DistQueue, LogQueue>::type q;
     __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
@@ -740,10 +801,10 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
         sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, par, nd, q, qout, &cn->qtail, pt,
-                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh);
+                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog);
         __syncthreads();
     }
-    bq_flush(q, qout, &cn->qtail);
+    q_flush(q, qout, plog, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
     publish_if_last(cn, pub, seq);
@@ -2108,6 +2169,23 @@ __device__ __forceinline__ u64 rec_state(const u64 *__restrict__ stt, const uint
     return stt[i];
 }
 
+// The push log into st (apply_logs): entry i of the log belongs to the first segment s with end[s] > i and
+// gets distance nd[s] (meta = end[0..nseg) then nd[0..nseg)).  Outside the timed region.
+__global__ __launch_bounds__(kBS) void k_resolve_log(const u64 *__restrict__ plog, int64_t n,
+                                                     const int64_t *__restrict__ meta, int nseg, u64 *__restrict__ stt) {
+    const int64_t *end = meta, *nd = meta + nseg;
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (end[mid] > i) hi = mid;
+            else lo = mid + 1;
+        }
+        const u64 e = plog[i];
+        stt[(uint32_t)e] = pack_state((uint32_t)(e >> 32), (int32_t)nd[lo]);
+    }
+}
+
 // st[v] = (par[v], nd_r) for every vertex v of every record r (the validator's and m_comp's view of a result;
 // a BFS with more than kMaxRec pull levels).  One wave per bitmap word, lane = bit: a word's par loads and state
 // stores are one coalesced access each.
@@ -2625,9 +2703,12 @@ bool has_hubs(const BfsWorkspace *ws) { return ws->hub_k > 0 || ws->hub_lim > 0;
 // the hub degree
 // skip_hubs (hybrid level): frontier vertices of the hub domain are left to the bottom-up hub sweep.
 // pub != null: the last kernel launched publishes the level's counters (seq) from its last workgroup
+// plog (single device): the level's winners go to the push log as vertex | parent << 32 at their queue positions
+// instead of a packed-state store (BfsWorkspace::plog)
 template <bool kDist>
 int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t dmax, int level, const Part &pt,
-              bool skip_hubs = false, Published *pub = nullptr, u64 seq = 0, uint32_t *par = nullptr) {
+              bool skip_hubs = false, Published *pub = nullptr, u64 seq = 0, uint32_t *par = nullptr,
+              u64 *plog = nullptr) {
     hipStream_t st = g->ctx->stream;
     const HubSet hs = hub_set(ws);
     const HubSet skip = skip_hubs ? hs : HubSet{0xFFFFFFFFu, 0u};
@@ -2645,21 +2726,21 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
                            ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
-                           hubs ? nullptr : pub, seq);
+                           hubs ? nullptr : pub, seq, plog);
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq);
+                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq, plog);
             BFSX_LAUNCHED(st);
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
-                           hubs ? nullptr : pub, seq);
+                           hubs ? nullptr : pub, seq, plog);
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq);
+                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq, plog);
             BFSX_LAUNCHED(st);
         }
     }
@@ -3023,6 +3104,8 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
     for (void *p : ws->prec) (void)hipFree(p);
     if (ws->par) (void)hipFree(ws->par);
+    if (ws->plog) (void)hipFree(ws->plog);
+    if (ws->d_log_meta) (void)hipFree(ws->d_log_meta);
     if (ws->h_err) (void)hipHostFree(ws->h_err);
     if (ws->ev_unpack0) (void)hipEventDestroy(ws->ev_unpack0);
     if (ws->ev_unpack1) (void)hipEventDestroy(ws->ev_unpack1);
@@ -3127,6 +3210,12 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t src_off[2];
     BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
 
+    // push log of this BFS (BfsWorkspace::plog), allocated once per workspace
+    ws->log_n = 0;
+    ws->log_end.clear();
+    ws->log_nd.clear();
+    ws->logs_pending = false;
+    if (opt.push_log && !ws->plog) BFSX_HIP_TRY(hipMalloc(&ws->plog, (size_t)std::max<int64_t>(nv, 1) * sizeof(u64)));
     const int64_t n_pre = ws->n_dead; // pre-visited non-padding ids
     if (opt.poison_queues) // test hook: a consumer that reads past a queue's tail meets 0xFFFFFFFF (id_ok)
         for (uint32_t *q : {ws->qa, ws->qb, ws->hubs})
@@ -3295,6 +3384,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         nh_found = -1;
         queue_ready = false;
         snapped = false;
+        u64 *plog = nullptr; // this level's push-log segment (a per-level push level with push_log)
         // level 0: a source row longer than persist_dmax enters K3p as its heavy table (row bounds known)
         const bool heavy_src = level == 0 && nf == 1 && dmax > opt.persist_dmax;
         if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax, heavy_src)) {
@@ -3346,7 +3436,9 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             const Part pt = single_part(g, ws);
             // test hook: the level's kernels read one entry past the queue's tail (the guard must catch it)
             const int64_t nf_l = level == opt.test_overread ? nf + 1 : nf;
-            if (int e = launch_td<false>(g, ws, nf_l, mf, dmax, level, pt, false, ws->d_pub, ++ws->pub_seq)) return e;
+            plog = opt.push_log ? ws->plog + ws->log_n : nullptr;
+            if (int e = launch_td<false>(g, ws, nf_l, mf, dmax, level, pt, false, ws->d_pub, ++ws->pub_seq, nullptr, plog))
+                return e;
             td_levels++;
         } else {
             // few unvisited candidates (the tail levels): the sparse kernel, which also queues its discoveries
@@ -3372,6 +3464,12 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         s.s2 = ws->h_pub->stage2;
         s.wk = ws->h_pub->walked;
         const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? ws->h_pub->qtail : s.nf;
+        if (plog && nf_new > 0) { // the level's winners are log entries [log_n, log_n + nf_new)
+            ws->log_n += nf_new;
+            ws->log_end.push_back(ws->log_n);
+            ws->log_nd.push_back(level + 1);
+            ws->logs_pending = true;
+        }
         const int rec_dir = sparse ? BFSX_DIR_BOTTOMUP_SPARSE : dir;
         g->level_dirs.push_back(rec_dir);
         bfsx_level_stat ls{};
@@ -3418,6 +3516,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     BFSX_HIP_TRY(hipEventSynchronize(ws->ev_end));
     if (int e = check_queue_guard(ws)) return e;
     recs.finish();
+    if (ws->logs_pending) ws->resolved = false;
     const int levels = level + 1;
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
@@ -3451,11 +3550,39 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
 
 } // namespace
 
-// Fold the last BFS's pull-level records into st (the validator's and m_comp's view of a result; outside
-// the timed region).  No-op when none is pending.
+// Scatter the last BFS's push log into st (outside the timed region; no-op when nothing is pending).  ev: recorded
+// after the segment table's upload, before the kernel (the unpack's timing starts there).
+int apply_logs(bfsx_graph *g, BfsWorkspace *ws, hipEvent_t ev = nullptr) {
+    hipStream_t st = g->ctx->stream;
+    const int nseg = (int)ws->log_end.size();
+    if (!ws->logs_pending || nseg == 0) {
+        ws->logs_pending = false;
+        if (ev) BFSX_HIP_TRY(hipEventRecord(ev, st));
+        return BFSX_OK;
+    }
+    if (2 * nseg > ws->log_meta_cap) {
+        if (ws->d_log_meta) BFSX_HIP_TRY(hipFree(ws->d_log_meta));
+        ws->log_meta_cap = std::max<int64_t>(2 * nseg, 256);
+        BFSX_HIP_TRY(hipMalloc(&ws->d_log_meta, ws->log_meta_cap * sizeof(int64_t)));
+    }
+    std::vector<int64_t> meta(ws->log_end);
+    meta.insert(meta.end(), ws->log_nd.begin(), ws->log_nd.end());
+    BFSX_HIP_TRY(hipMemcpyAsync(ws->d_log_meta, meta.data(), meta.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    BFSX_HIP_TRY(hipStreamSynchronize(st)); // meta is a host temporary
+    if (ev) BFSX_HIP_TRY(hipEventRecord(ev, st));
+    hipLaunchKernelGGL(k_resolve_log, dim3(clamp_grid((ws->log_n + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->plog,
+                       ws->log_n, ws->d_log_meta, nseg, ws->st);
+    BFSX_LAUNCHED(st);
+    ws->logs_pending = false;
+    return BFSX_OK;
+}
+
+// Fold the last BFS's pull-level records and push log into st (the validator's and m_comp's view of a result;
+// outside the timed region).  No-op when none is pending.
 int bfs_resolve(bfsx_graph *g) {
     BfsWorkspace *ws = g->ws;
     if (!ws || ws->resolved) return BFSX_OK;
+    if (int e = apply_logs(g, ws)) return e;
     hipStream_t st = g->ctx->stream;
     RecSet rs{};
     rs.n = ws->n_prec;
@@ -3555,7 +3682,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
         src_dead = (dw >> (src & 63)) & 1ull;
     }
-    BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack0, st));
+    if (int e = apply_logs(g, ws, ws->ev_unpack0)) return e; // the push log is part of the unpack's time
     if (gather) {
         hipLaunchKernelGGL(k_unpack_gather, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_perm, g->d_inv,
                            (int64_t)nv, ws->dead, src, ws->out64, d_dist_only);

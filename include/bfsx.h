@@ -100,6 +100,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
  *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS)
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
+ *   "push_log" = on|off (one device: a per-level push level writes its winners as (vertex, parent) pairs at
+ *                 their queue positions instead of scattered state stores; the result read scatters them;
+ *                 default on)
  *   "persist_blocks" = auto|int (workgroups of that launch, auto = three per four CUs (192 on MI355X), capped
  *                 by the occupancy API so that every workgroup is resident; fixed at a graph's first BFS)
  *   "pull_min_edges" = int (a push -> pull switch also needs the frontier to hold at least this many edges,

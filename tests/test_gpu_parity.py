@@ -262,6 +262,42 @@ def test_persistent_topdown_matches_per_level_kernels(ctx, case, blocks):
         assert res["on", src] == res["off", src]
 
 
+@pytest.mark.parametrize("persist", ["off", "on"])
+def test_push_log_matches_state_stores(ctx, persist):
+    """push_log (per-level push winners as (vertex, parent) pairs at their queue positions, scattered into the
+    state when the result is read) against the packed-state stores: identical distances and a valid parent
+    tree, through every reader of the result -- bfsx_bfs's arrays, bfsx_result after another BFS ran, the
+    device validator and m_comp -- on a Kronecker graph (hub-bin push levels, pull levels, hybrid levels) and
+    a grid (many narrow push levels; persist off puts them all in the per-level kernels)."""
+    cases = []
+    u, v = O.kronecker(14, 16, 7)
+    cases.append((1 << 14, np.asarray(u, np.uint32), np.asarray(v, np.uint32)))
+    side = 90
+    idx = np.arange(side * side).reshape(side, side)
+    cases.append((side * side, np.r_[idx[:, :-1].ravel(), idx[:-1, :].ravel()].astype(np.uint32),
+                  np.r_[idx[:, 1:].ravel(), idx[1:, :].ravel()].astype(np.uint32)))
+    try:
+        ctx.set_option("persist", persist)
+        for nv, u, v in cases:
+            off, col = O.build_sets(nv, u, v)
+            srcs = [int(u[0]), int(v[len(v) // 3]), int(u[-1])]
+            refs = [O.csr_bfs(nv, off, col, s)[0] for s in srcs]
+            for mode in ("off", "on"):
+                ctx.set_option("push_log", mode)
+                with ctx.from_edges(nv, u, v) as g:
+                    for src, ref in zip(srcs, refs):
+                        d, p, st = g.bfs(src)
+                        assert np.array_equal(d, ref), (mode, src)
+                        assert O.validate(nv, off, col, src, d, p) == 0
+                        assert g.validate()["errors"] == 0
+                    # the result of the last BFS read again, after the validator resolved it
+                    d2, p2 = g.result()
+                    assert np.array_equal(d2, refs[-1]) and np.array_equal(p2, p)
+    finally:
+        ctx.set_option("push_log", "on")
+        ctx.set_option("persist", "on")
+
+
 @pytest.mark.parametrize("abort_at", [0, 3])
 def test_persistent_abort_falls_back(ctx, abort_at):
     """A K3p launch whose grid barrier gives up (here: the "persist_abort_at" hook, the same exit path a
