@@ -4229,6 +4229,12 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     }
     int64_t deg_local = 0;
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st)); // before the timed region
+    // the partitioned loop keeps the packed-state stores (no push log): a stale log of an earlier one-device BFS
+    // on this workspace must not be applied to this result
+    ws->log_n = 0;
+    ws->log_end.clear();
+    ws->log_nd.clear();
+    ws->logs_pending = false;
     if ((rc = dist_begin(g, source, &deg_local, deg))) return rc;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
