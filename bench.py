@@ -431,7 +431,8 @@ def run_single(args):
                 "t_unpack_ms": round(float(np.mean(unpack_ms)), 4),
                 "value_with_output": hmean(with_out),
                 "t_result_copy_ms": round(float(np.mean(d2h_ms)), 3),
-                "output_note": "t_unpack_ms: device time of the unpack kernel (internal-id state + the pull levels' "
+                "output_note": "t_unpack_ms: device time of the result materialisation (the push levels' log "
+                               "scattered into the internal-id state, then the gather of state + the pull levels' "
                                "records -> one (parent, dist) word per original id), outside t_bfs, mean over the "
                                "roots; value_with_output: harmonic-mean GTEPS over t_bfs + t_unpack (the promised "
                                "output materialised on the device); t_result_copy_ms: host wall time of bfsx_result "
