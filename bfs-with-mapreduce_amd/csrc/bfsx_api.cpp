@@ -148,9 +148,17 @@ int to_internal(const bfsx_graph *g, int64_t v, int64_t *out) {
         return BFSX_OK;
     }
     if (v < g->v_lo || v >= g->v_lo + g->nv) return fail(BFSX_E_ARG, "vertex not owned by this rank");
+    auto &memo = const_cast<bfsx_graph *>(g)->perm_memo;
+    const auto it = memo.find(v);
+    if (it != memo.end()) {
+        *out = it->second;
+        return BFSX_OK;
+    }
     uint32_t x = 0;
     BFSX_HIP_TRY(hipMemcpy(&x, g->d_perm + (v - g->v_lo), sizeof(x), hipMemcpyDeviceToHost));
     *out = g->v_lo + (int64_t)x;
+    if (memo.size() >= 65536) memo.clear();
+    memo.emplace(v, *out);
     return BFSX_OK;
 }
 

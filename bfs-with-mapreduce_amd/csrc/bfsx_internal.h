@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../include/bfsx.h"
@@ -163,6 +165,10 @@ struct bfsx_graph {
     // internal id; perm[original] = internal, inv[internal] = original.  Null: internal = original.
     uint32_t *d_perm = nullptr, *d_inv = nullptr;
     bfsx::BfsWorkspace *ws = nullptr;
+    // host memo of the immutable per-source lookups a BFS start reads back from the device (each a synchronous
+    // 4-16 B copy, ~10 us of host time): original -> internal id, internal id -> its row bounds.  Bounded.
+    std::unordered_map<int64_t, int64_t> perm_memo;
+    std::unordered_map<int64_t, std::pair<int64_t, int64_t>> row_memo;
     // most recent BFS
     int64_t last_source = -1;
     double last_t_bfs_ms = 0.0; // device time of the most recent BFS (source init -> finalize)

@@ -3208,7 +3208,15 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     const unsigned cap = (unsigned)ctx->num_cus * 8u;
 
     int64_t src_off[2];
-    BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
+    const auto rm = g->row_memo.find(source);
+    if (rm != g->row_memo.end()) {
+        src_off[0] = rm->second.first;
+        src_off[1] = rm->second.second;
+    } else {
+        BFSX_HIP_TRY(hipMemcpy(src_off, g->d_row_off + source, sizeof(src_off), hipMemcpyDeviceToHost));
+        if (g->row_memo.size() >= 65536) g->row_memo.clear();
+        g->row_memo.emplace(source, std::make_pair(src_off[0], src_off[1]));
+    }
 
     // push log of this BFS (BfsWorkspace::plog), allocated once per workspace
     ws->log_n = 0;
