@@ -260,6 +260,14 @@ __device__ inline u64 wave_max(u64 x) {
     }
     return x;
 }
+__device__ inline uint32_t wave_max32(uint32_t x) { // one lane exchange per step where u64 takes two
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t y = __shfl_xor(x, d);
+        x = y > x ? y : x;
+    }
+    return x;
+}
 
 __device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu, u64 dmax = 0,
                                  u64 stage2 = 0, u64 walked = 0, u64 nhub = 0) {
@@ -1055,7 +1063,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             }
             if (tid == kBS - 1) s_hscan[kHeavyMax] = run;
         }
-        const uint32_t vb = (uint32_t)((u64)nf * b / G), ve = (uint32_t)((u64)nf * (b + 1) / G);
+        // nf <= kPersistNf and b < kBS: the products fit 32 bits (no 64-bit division on the critical path)
+        const uint32_t vb = nf * b / G, ve = nf * (b + 1) / G;
         __syncthreads();
         // light rows: this workgroup's slice of the frontier, its rows swept by this workgroup
         for (uint32_t base = vb; base < ve; base += kBS) {
@@ -1236,9 +1245,19 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                 }
             }
         }
+        // what every workgroup needs for the offsets and the stop decision; the statistics only workgroup 0
+        // publishes (scanned, claims, hub m_f, heavy d_max) are reduced there alone (the level's critical path)
+        const bool stats = b == 0;
         const uint32_t inc = wave_incl_scan((uint32_t)r_n), hinc = kHeavy ? wave_incl_scan((uint32_t)r_nh) : 0u;
-        const u64 smf = wave_sum(r_mf), ssc = wave_sum(r_sc), scl = wave_sum(r_cl), sdm = wave_max(r_dm),
-                  smfh = wave_sum(r_mfh), seh = kHeavy ? wave_sum(r_eh) : 0ull, sdmh = kHeavy ? wave_max(r_dmh) : 0ull;
+        const u64 smf = wave_sum(r_mf), seh = kHeavy ? wave_sum(r_eh) : 0ull;
+        const u64 sdm = wave_max32((uint32_t)r_dm); // d_max values are clamped to 24 bits
+        u64 ssc = 0, scl = 0, smfh = 0, sdmh = 0;
+        if (stats) {
+            ssc = wave_sum(r_sc);
+            scl = wave_sum(r_cl);
+            smfh = wave_sum(r_mfh);
+            sdmh = kHeavy ? wave_max(r_dmh) : 0ull;
+        }
         __shared__ uint32_t s_hw[kWaves];
         __syncthreads(); // s_red / s_wsum reuse
         if (lane == 63) {
@@ -1264,12 +1283,14 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             hoff += (w < (int)wave) ? s_hw[w] : 0u;
             nh_new += s_hw[w];
             mf_new += s_red[0][w];
-            sc_new += s_red[1][w];
-            cl_new += s_red[2][w];
             dm_new = s_red[3][w] > dm_new ? s_red[3][w] : dm_new;
-            mfh_new += s_red[4][w];
             eh_new += s_red[5][w];
-            dmh_new = s_red[6][w] > dmh_new ? s_red[6][w] : dmh_new;
+            if (stats) {
+                sc_new += s_red[1][w];
+                cl_new += s_red[2][w];
+                mfh_new += s_red[4][w];
+                dmh_new = s_red[6][w] > dmh_new ? s_red[6][w] : dmh_new;
+            }
         }
         const uint32_t my_n = (uint32_t)r_n, my_nh = (uint32_t)r_nh;
         s_off[tid] = woff + inc - my_n; // entries past G: unused
@@ -1294,9 +1315,12 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         // stop when the BFS ends, the light frontier is no longer narrow, the heavy table would overflow, a
         // workgroup's share (light slice + heavy edges) could overflow its segment, Beamer asks for
         // bottom-up, or the level budget is used up
+        // (Beamer's m_f > m_u / alpha as a product: the same decision as the host's for m_u >= 0, without a
+        // 64-bit division on every workgroup's critical path)
+        const bool beamer = alpha > 0 && (mu >= 0 ? (int64_t)mf_new * alpha > mu : (int64_t)mf_new > mu / alpha);
         const bool stop = nf_all == 0 || nf_new > kPersistNf || nh_new > kHeavyMax ||
-                          (u64)((nf_new + G - 1) / G) * dm_new + (eh_new + G - 1) / G > (u64)kRegion ||
-                          (alpha > 0 && (int64_t)mf_new > mu / alpha && (int64_t)mf_new > bu_floor) ||
+                          (u64)((nf_new + G - 1) / G) * dm_new + (kHeavy ? (eh_new + G - 1) / G : 0ull) > (u64)kRegion ||
+                          (beamer && (int64_t)mf_new > bu_floor) ||
                           it + 1 >= max_levels;
         __syncthreads();
         // the host reads the counts as soon as they are final (a mapped flag, no stream synchronise: that cost ~13 us
