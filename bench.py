@@ -95,7 +95,29 @@ def parse_args():
     ap.add_argument("--levels-json", default="")
     ap.add_argument("--option", action="append", default=[], help="libbfsx option key=value")
     ap.add_argument("--dist", action="store_true", help="use the partitioned path even on one rank (rehearsal)")
+    ap.add_argument("--deadline", type=float, default=900.0,
+                    help="seconds after which a rank (and the --gpus N launcher) gives up and exits 124 instead of "
+                         "waiting on a stuck peer (0: none)")
     return ap.parse_args()
+
+
+def arm_deadline(seconds, what):
+    """End this process with exit code 124 when it still runs after `seconds`.  Every rank arms it: a rank stuck
+    behind a failed or diverged peer must not burn the driver's time limit and leave no JSON line (libbfsx also
+    fails every rank's call when one rank fails, and gives up a collective after comm_timeout_ms; this is the
+    last line).  torch.distributed.run then stops the other ranks."""
+    if seconds <= 0:
+        return None
+    import threading
+
+    def fire():
+        print(f"[bench] {what}: deadline of {seconds:.0f} s passed, exiting 124", file=sys.stderr, flush=True)
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def pick_roots(args, g, m_tuples, bfs_mcomp, validate):
@@ -472,6 +494,7 @@ def run_dist(args, world, rank, local_rank):
     import torch
     import torch.distributed as dist
 
+    arm_deadline(args.deadline, f"rank {rank} of {world}")
     # Gloo and RCCL print banners on the process's C-level stdout; the contract is ONE JSON line, so
     # fd 1 points at stderr until the result is printed
     sys.stdout.flush()
@@ -570,7 +593,22 @@ def launch_ranks(args):
            "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
            os.path.abspath(__file__)] + sys.argv[1:]
     print(f"[bench] --gpus {args.gpus}: launching {' '.join(cmd)}", file=sys.stderr, flush=True)
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    # the ranks arm --deadline themselves; this bound (a minute later) also covers a launcher that hangs, and
+    # takes the whole process group (the launcher and every rank) down with it
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=args.deadline + 60 if args.deadline > 0 else None)
+    except subprocess.TimeoutExpired:
+        import signal
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        print(f"[bench] ranks still running {args.deadline + 60:.0f} s after the launch: killed", file=sys.stderr,
+              flush=True)
+        return 124
+
+    class R:
+        returncode, stdout = p.returncode, out
+    r = R
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     js = [ln for ln in lines if ln.lstrip().startswith("{")]
     for ln in lines:

@@ -37,7 +37,7 @@ EXPORTS = [
     "bfsx_device_synchronize", "bfsx_validate", "bfsx_validate_result",
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
     "bfsx_last_bfs_ms", "bfsx_last_unpack_ms", "bfsx_persist_fallbacks", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group",
-    "bfsx_dist_bfs",
+    "bfsx_dist_bfs", "bfsx_init_group", "bfsx_group_size", "bfsx_dist_graph_load_algs4",
 ]
 # test-only level primitives (include/bfsx_levels.h): exported for tests/dist_driver.py, not product ABI
 TEST_EXPORTS = [
@@ -137,6 +137,9 @@ def lib():
         L.bfsx_comm_init.argtypes = [_VP, C.c_int, C.c_int, _VP]
         L.bfsx_comm_local_group.argtypes = [_VP, C.c_int]
         L.bfsx_dist_bfs.argtypes = [_VP, C.c_int64, C.POINTER(Stats)]
+        L.bfsx_init_group.argtypes = [C.c_int, C.POINTER(_VP)]
+        L.bfsx_group_size.argtypes = [_VP]
+        L.bfsx_dist_graph_load_algs4.argtypes = [_VP, C.c_char_p, C.c_int, C.c_int, C.POINTER(_VP)]
         _lib = L
     return _lib
 
@@ -181,14 +184,22 @@ def parse_algs4(path):
 
 
 class Context:
-    """One device (bfsx_init .. bfsx_finalize)."""
+    """One device (bfsx_init .. bfsx_finalize), or with group=N a group context of N ranks in this process
+    (bfsx_init_group): graphs built on it are partitioned over the ranks, and every call runs all of them."""
 
-    def __init__(self, device=0, **options):
+    def __init__(self, device=0, group=None, **options):
         h = _VP()
-        _check(lib().bfsx_init(device, C.byref(h)))
+        if group is not None:
+            _check(lib().bfsx_init_group(int(group), C.byref(h)))
+        else:
+            _check(lib().bfsx_init(device, C.byref(h)))
         self._h = h
         for k, val in options.items():
             self.set_option(k, val)
+
+    @property
+    def group_size(self):
+        return lib().bfsx_group_size(self._h)
 
     def set_option(self, key, value):
         _check(lib().bfsx_set_option(self._h, key.encode(), str(value).encode()))
@@ -232,6 +243,11 @@ class Context:
         _check(lib().bfsx_dist_graph_from_edges(self._h, nv, _p(u), _p(v), len(u), rank, nranks, C.byref(g)))
         return Graph(self, g)
 
+    def dist_load_algs4(self, path, rank, nranks):
+        g = _VP()
+        _check(lib().bfsx_dist_graph_load_algs4(self._h, os.fsencode(path), rank, nranks, C.byref(g)))
+        return Graph(self, g)
+
     def dist_kronecker(self, scale, rank, nranks, edgefactor=16, seed=0x5EED2026):
         g = _VP()
         _check(lib().bfsx_dist_graph_kronecker(self._h, scale, edgefactor, seed, rank, nranks, C.byref(g)))
@@ -249,7 +265,8 @@ class Context:
 
     def comm_init(self, rank, nranks, uid):
         """Collective over the nranks processes: attach an RCCL communicator to this context."""
-        assert len(uid) == COMM_ID_BYTES
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"an RCCL unique id has {COMM_ID_BYTES} bytes")
         buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
         _check(lib().bfsx_comm_init(self._h, rank, nranks, buf))
 
@@ -342,8 +359,14 @@ class Graph:
             dist = np.empty(self.nv, np.int32)
         if parent is None and want_parent:
             parent = np.empty(self.nv, np.int64)
-        assert dist.dtype == np.int32 and dist.size == self.nv and dist.flags.c_contiguous
-        assert parent is None or (parent.dtype == np.int64 and parent.size == self.nv and parent.flags.c_contiguous)
+        # explicit checks (not asserts, which python -O drops): bfsx_result writes nv elements into both arrays
+        if not (isinstance(dist, np.ndarray) and dist.dtype == np.int32 and dist.size == self.nv
+                and dist.flags.c_contiguous and dist.flags.writeable):
+            raise ValueError(f"dist must be a writeable C-contiguous int32 array of {self.nv} elements")
+        if parent is not None and not (isinstance(parent, np.ndarray) and parent.dtype == np.int64
+                                       and parent.size == self.nv and parent.flags.c_contiguous
+                                       and parent.flags.writeable):
+            raise ValueError(f"parent must be a writeable C-contiguous int64 array of {self.nv} elements")
         _check(lib().bfsx_result(self._h, _p(dist), _p(parent)))
         return dist, parent
 
@@ -359,7 +382,8 @@ class Graph:
         """Validate a caller-supplied (dist, parent) for this graph's rows.  Returns (errors, first_bad)."""
         dist = np.ascontiguousarray(dist, np.int32)
         parent = np.ascontiguousarray(parent, np.int64)
-        assert len(dist) == self.nv and len(parent) == self.nv
+        if len(dist) != self.nv or len(parent) != self.nv:
+            raise ValueError(f"dist and parent must hold {self.nv} elements")
         e, f = C.c_int64(), C.c_int64()
         _check(lib().bfsx_validate_result(self._h, source, _p(dist), _p(parent), C.byref(e), C.byref(f)))
         return e.value, f.value

@@ -9,12 +9,15 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_set>
 
 #include "../../include/bfsx_levels.h"
@@ -31,6 +34,8 @@ int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
 }
+
+const std::string &last_error() { return g_last_error; }
 
 namespace {
 
@@ -181,6 +186,90 @@ int to_original(const bfsx_graph *g, int64_t x, int64_t *out) {
     return BFSX_OK;
 }
 
+// ---- group contexts (bfsx_init_group): N ranks of one process, one host thread per rank ------------------
+// "Multi-GPU is internal: one host thread (or process) per device, with an RCCL communicator
+// per ctx.  The caller sees one call."  Every call on a group context or graph runs the rank calls of the
+// 1-D partitioned path (bfsx_dist_*) on one host thread per rank and returns when all have finished.
+namespace {
+
+bool is_group(const bfsx_ctx *c) { return c && !c->ranks.empty(); }
+bool is_group(const bfsx_graph *g) { return g && !g->parts.empty(); }
+
+// fn(r) on one host thread per rank (rank r's device current).  The reported error is the first rank whose
+// failure is its own -- a rank that only saw a peer abort the group says "peer rank ..." -- prefixed with its rank.
+int run_ranks(const std::vector<bfsx_ctx *> &ranks, const std::function<int(int)> &fn) {
+    const int P = (int)ranks.size();
+    std::vector<int> rc(P, BFSX_OK);
+    std::vector<std::string> msg(P);
+    std::vector<std::thread> th;
+    th.reserve(P);
+    for (int r = 0; r < P; r++)
+        th.emplace_back([&, r] {
+            const hipError_t he = hipSetDevice(ranks[r]->device);
+            rc[r] = he != hipSuccess ? fail(BFSX_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)) : fn(r);
+            if (rc[r]) msg[r] = last_error();
+        });
+    for (auto &t : th) t.join();
+    int pick = -1;
+    auto peer = [&](int r) { return msg[r].rfind("peer rank", 0) == 0; };
+    for (int r = 0; r < P; r++)
+        if (rc[r] && (pick < 0 || (peer(pick) && !peer(r)))) pick = r;
+    if (pick < 0) return BFSX_OK;
+    return fail(rc[pick], "rank " + std::to_string(pick) + ": " + msg[pick]);
+}
+
+// a group graph from every rank's partition (graph construction has no collective: a failed rank fails alone)
+int group_graph(bfsx_ctx *ctx, bfsx_graph **out, const std::function<int(int, bfsx_graph **)> &make) {
+    const int P = (int)ctx->ranks.size();
+    std::vector<bfsx_graph *> parts(P, nullptr);
+    const int rc = run_ranks(ctx->ranks, [&](int r) { return make(r, &parts[r]); });
+    if (rc) {
+        for (bfsx_graph *p : parts) bfsx_graph_free(p);
+        return rc;
+    }
+    auto *g = new (std::nothrow) bfsx_graph();
+    if (!g) {
+        for (bfsx_graph *p : parts) bfsx_graph_free(p);
+        return fail(BFSX_E_OOM, "graph");
+    }
+    g->ctx = ctx;
+    g->parts = parts;
+    g->nranks = P;
+    g->nv_global = g->nv = parts[0]->nv_global;
+    g->chunk = parts[0]->chunk;
+    g->m = parts[0]->m;
+    for (bfsx_graph *p : parts) g->nnz += p->nnz;
+    *out = g;
+    return BFSX_OK;
+}
+
+int group_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (source < 0 || source >= g->nv_global)
+        return fail(BFSX_E_RANGE, "source vertex " + std::to_string(source) + " outside [0, " +
+                                      std::to_string(g->nv_global) + ")");
+    const int P = (int)g->parts.size();
+    std::vector<bfsx_stats> st(P);
+    const int rc = run_ranks(g->ctx->ranks, [&](int r) {
+        bfsx_graph *p = g->parts[r];
+        if (int e = dist_bfs_run(p, source, stats ? &st[r] : nullptr)) return e;
+        if (!dist_out && !parent_out) return BFSX_OK;
+        return bfs_copy_result(p, dist_out ? dist_out + p->v_lo : nullptr, parent_out ? parent_out + p->v_lo : nullptr);
+    });
+    if (rc) return rc;
+    g->last_source = source;
+    g->last_t_bfs_ms = 0;
+    for (bfsx_graph *p : g->parts) g->last_t_bfs_ms = std::max(g->last_t_bfs_ms, p->last_t_bfs_ms);
+    if (stats) {
+        *stats = st[0]; // levels, directions and the all-reduced m_comp / reached agree on every rank
+        stats->t_bfs_ms = g->last_t_bfs_ms;
+        stats->t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return BFSX_OK;
+}
+
+} // namespace
+
 } // namespace bfsx
 
 using namespace bfsx;
@@ -251,16 +340,57 @@ int bfsx_init(int device, bfsx_ctx **out) {
     return BFSX_OK;
 }
 
+int bfsx_init_group(int nranks, bfsx_ctx **out) {
+    if (!out || nranks < 1 || nranks > 64) return fail(BFSX_E_ARG, "nranks must be in [1, 64]");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(BFSX_E_NODEV, "no HIP device available");
+    const char *mode = std::getenv("BFSX_GROUP_COMM"); // rccl | local (default: rccl when the devices are distinct)
+    const bool want_local = mode && !std::strcmp(mode, "local");
+    if (mode && !std::strcmp(mode, "rccl") && nranks > count)
+        return fail(BFSX_E_ARG, "BFSX_GROUP_COMM=rccl needs one device per rank (" + std::to_string(count) + " visible)");
+    auto *gctx = new (std::nothrow) bfsx_ctx();
+    if (!gctx) return fail(BFSX_E_OOM, "ctx");
+    for (int r = 0; r < nranks; r++) {
+        bfsx_ctx *c = nullptr;
+        if (int rc = bfsx_init(r % count, &c)) {
+            bfsx_finalize(gctx);
+            return rc;
+        }
+        gctx->ranks.push_back(c);
+    }
+    gctx->num_cus = gctx->ranks[0]->num_cus;
+    if (int rc = comm_clique(gctx->ranks.data(), nranks, nranks <= count && !want_local)) {
+        const std::string msg = last_error();
+        bfsx_finalize(gctx);
+        return fail(rc, msg);
+    }
+    *out = gctx;
+    return BFSX_OK;
+}
+
+int bfsx_group_size(const bfsx_ctx *ctx) { return !ctx ? BFSX_E_ARG : is_group(ctx) ? (int)ctx->ranks.size() : 1; }
+
 void bfsx_finalize(bfsx_ctx *ctx) {
     if (!ctx) return;
+    for (bfsx_ctx *c : ctx->ranks) bfsx_finalize(c);
+    ctx->ranks.clear();
     (void)hipSetDevice(ctx->device);
     ctx->comm.reset();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
+static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value);
+
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
     if (!ctx || !key || !value) return fail(BFSX_E_ARG, "null argument");
+    if (int rc = set_option_one(ctx, key, value)) return rc;
+    for (bfsx_ctx *c : ctx->ranks) // a group context: every rank's
+        if (int rc = set_option_one(c, key, value)) return rc;
+    return BFSX_OK;
+}
+
+static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
     const std::string k(key), v(value);
     auto as_int = [&](int &dst) -> int {
         char *end = nullptr;
@@ -376,6 +506,40 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
         if (v == "on") ctx->opt.check_retired = true;
         else if (v == "off") ctx->opt.check_retired = false;
         else return fail(BFSX_E_ARG, "check_retired must be on|off");
+        return BFSX_OK;
+    }
+    if (k == "check_collectives") {
+        if (v == "on") ctx->opt.check_collectives = true;
+        else if (v == "off") ctx->opt.check_collectives = false;
+        else return fail(BFSX_E_ARG, "check_collectives must be on|off");
+        comm_sync_options(ctx);
+        return BFSX_OK;
+    }
+    if (k == "comm_timeout_ms") {
+        char *end = nullptr;
+        const long long x = strtoll(value, &end, 10);
+        if (!end || *end || x < 0) return fail(BFSX_E_ARG, "comm_timeout_ms must be a duration >= 0 (0: no deadline)");
+        ctx->opt.comm_timeout_ms = x;
+        comm_sync_options(ctx);
+        return BFSX_OK;
+    }
+    if (k == "fail_at") { // test hook: "rank:level", "rank:setup" or "off"
+        if (v == "off") {
+            ctx->opt.fail_rank = ctx->opt.fail_level = -1;
+            return BFSX_OK;
+        }
+        const size_t c = v.find(':');
+        char *end = nullptr;
+        const long r = c == std::string::npos ? -1 : strtol(v.substr(0, c).c_str(), &end, 10);
+        if (r < 0 || r >= 64 || !end || *end) return fail(BFSX_E_ARG, "fail_at must be off|rank:level|rank:setup");
+        const std::string l = v.substr(c + 1);
+        long lv = -2;
+        if (l != "setup") {
+            lv = strtol(l.c_str(), &end, 10);
+            if (l.empty() || !end || *end || lv < 0) return fail(BFSX_E_ARG, "fail_at must be off|rank:level|rank:setup");
+        }
+        ctx->opt.fail_rank = (int)r;
+        ctx->opt.fail_level = (int)lv;
         return BFSX_OK;
     }
     if (k == "leaf_skip") {
@@ -500,6 +664,7 @@ static int graph_from_device_edges(bfsx_ctx *ctx, int64_t nv, uint32_t *d_u, uin
 static int graph_from_host_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
                                  int rank, int nranks, bfsx_graph **out, bool dist) {
     if (!ctx || !out || nv <= 0 || m < 0 || (m > 0 && (!u || !v))) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(ctx)) return fail(BFSX_E_ARG, "a group context partitions its graphs itself (bfsx_graph_from_edges)");
     if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
     if (nv > (int64_t)INT32_MAX) return fail(BFSX_E_ARG, "nv must be < 2^31 on one device");
     for (int64_t i = 0; i < m; i++)
@@ -528,6 +693,13 @@ static int graph_from_host_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, c
 
 int bfsx_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, const uint32_t *v, int64_t m,
                           bfsx_graph **out) {
+    if (is_group(ctx)) {
+        if (!out) return fail(BFSX_E_ARG, "null out");
+        const int P = (int)ctx->ranks.size();
+        return group_graph(ctx, out, [&](int r, bfsx_graph **o) {
+            return graph_from_host_edges(ctx->ranks[r], nv, u, v, m, r, P, o, true);
+        });
+    }
     return graph_from_host_edges(ctx, nv, u, v, m, 0, 1, out, false);
 }
 
@@ -536,8 +708,30 @@ int bfsx_dist_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, con
     return graph_from_host_edges(ctx, nv, u, v, m, rank, nranks, out, true);
 }
 
+int bfsx_dist_graph_load_algs4(bfsx_ctx *ctx, const char *path, int rank, int nranks, bfsx_graph **out) {
+    if (!ctx || !path || !out || is_group(ctx)) return fail(BFSX_E_ARG, "bad argument");
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
+    int64_t nv = 0, m = 0;
+    uint32_t *d_u = nullptr, *d_v = nullptr;
+    // every rank tokenizes the whole file on its own device (kernels_parse.hip) and keeps the rows it owns
+    int rc = load_algs4_device(ctx, path, nv, m, d_u, d_v);
+    if (rc) return rc;
+    if (nv > (int64_t)INT32_MAX) rc = fail(BFSX_E_ARG, "nv must be < 2^31");
+    if (!rc) rc = graph_from_device_edges(ctx, nv, d_u, d_v, m, rank, nranks, out, true);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    return rc;
+}
+
 int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
     if (!ctx || !path || !out) return fail(BFSX_E_ARG, "null argument");
+    if (is_group(ctx)) {
+        const int P = (int)ctx->ranks.size();
+        return group_graph(ctx, out, [&](int r, bfsx_graph **o) {
+            return bfsx_dist_graph_load_algs4(ctx->ranks[r], path, r, P, o);
+        });
+    }
     int64_t nv = 0, m = 0;
     uint32_t *d_u = nullptr, *d_v = nullptr;
     int rc = load_algs4_device(ctx, path, nv, m, d_u, d_v);
@@ -553,6 +747,7 @@ int bfsx_graph_load_algs4(bfsx_ctx *ctx, const char *path, bfsx_graph **out) {
 int bfsx_parse_algs4_gpu(bfsx_ctx *ctx, const char *path, int64_t *nv_out, int64_t *m_out, uint32_t **u_out,
                          uint32_t **v_out) {
     if (!ctx || !path || !nv_out || !m_out || !u_out || !v_out) return fail(BFSX_E_ARG, "null argument");
+    if (is_group(ctx)) ctx = ctx->ranks[0];
     int64_t nv = 0, m = 0;
     uint32_t *d_u = nullptr, *d_v = nullptr;
     int rc = load_algs4_device(ctx, path, nv, m, d_u, d_v);
@@ -580,6 +775,7 @@ int bfsx_parse_algs4_gpu(bfsx_ctx *ctx, const char *path, int64_t *nv_out, int64
 
 int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, uint32_t *u, uint32_t *v) {
     if (!ctx || !u || !v || scale < 1 || scale > 31 || edgefactor < 1) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(ctx)) ctx = ctx->ranks[0];
     BFSX_HIP_TRY(hipSetDevice(ctx->device));
     const int64_t m = (int64_t)edgefactor << scale;
     uint32_t *d_u = nullptr, *d_v = nullptr;
@@ -601,6 +797,13 @@ int bfsx_kronecker_edges(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed
 static int graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
                            bfsx_graph **out, bool dist) {
     if (!ctx || !out || scale < 1 || scale > 30 || edgefactor < 1) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(ctx)) {
+        if (dist) return fail(BFSX_E_ARG, "a group context partitions its graphs itself (bfsx_graph_kronecker)");
+        const int P = (int)ctx->ranks.size();
+        return group_graph(ctx, out, [&](int r, bfsx_graph **o) {
+            return graph_kronecker(ctx->ranks[r], scale, edgefactor, seed, r, P, o, true);
+        });
+    }
     if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return fail(BFSX_E_ARG, "bad rank/nranks");
     BFSX_HIP_TRY(hipSetDevice(ctx->device));
     const int64_t nv = (int64_t)1 << scale;
@@ -634,6 +837,15 @@ int bfsx_dist_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t
 int bfsx_graph_partition(const bfsx_graph *g, int64_t *nv_global, int64_t *v_lo, int64_t *nv_local, int64_t *chunk,
                          int32_t *rank, int32_t *nranks) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (is_group(g)) { // the whole graph, held by nranks ranks of this process
+        if (nv_global) *nv_global = g->nv_global;
+        if (v_lo) *v_lo = 0;
+        if (nv_local) *nv_local = g->nv_global;
+        if (chunk) *chunk = g->chunk;
+        if (rank) *rank = 0;
+        if (nranks) *nranks = (int32_t)g->parts.size();
+        return BFSX_OK;
+    }
     if (nv_global) *nv_global = g->nv_global;
     if (v_lo) *v_lo = g->v_lo;
     if (nv_local) *nv_local = g->nv;
@@ -646,11 +858,19 @@ int bfsx_graph_partition(const bfsx_graph *g, int64_t *nv_global, int64_t *v_lo,
 #define BFSX_DIST_GUARD(g)                                                                           \
     do {                                                                                             \
         if (!(g)) return fail(BFSX_E_ARG, "null graph");                                             \
+        if (is_group(g)) return fail(BFSX_E_ARG, "a group graph runs its ranks itself: use bfsx_bfs"); \
         BFSX_HIP_TRY(hipSetDevice((g)->ctx->device));                                                \
     } while (0)
 
 int bfsx_graph_degree(const bfsx_graph *g, int64_t v, int64_t *deg) {
     if (!g || !deg) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) {
+        if (v < 0 || v >= g->nv_global) {
+            *deg = -1;
+            return BFSX_OK;
+        }
+        return bfsx_graph_degree(g->parts[(size_t)(v / g->chunk)], v, deg);
+    }
     *deg = -1;
     if (v < g->v_lo || v >= g->v_lo + g->nv) return BFSX_OK;
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
@@ -733,6 +953,8 @@ int bfsx_dist_mcomp(bfsx_graph *g, int64_t *m_local, int64_t *reached_local) {
 
 void bfsx_graph_free(bfsx_graph *g) {
     if (!g) return;
+    for (bfsx_graph *p : g->parts) bfsx_graph_free(p);
+    g->parts.clear();
     (void)hipSetDevice(g->ctx->device);
     bfs_workspace_free(g->ws);
     if (g->d_row_off) (void)hipFree(g->d_row_off);
@@ -749,6 +971,18 @@ int64_t bfsx_graph_m(const bfsx_graph *g) { return g ? g->m : -1; }
 
 int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (is_group(g)) { // the ranks' rows in id order, one after the other
+        int64_t base = 0;
+        for (const bfsx_graph *p : g->parts) {
+            std::vector<int64_t> off((size_t)p->nv + 1);
+            BFSX_HIP_TRY(hipSetDevice(p->ctx->device));
+            if (int rc = bfsx_graph_csr(p, off.data(), col ? col + base : nullptr)) return rc;
+            if (row_off)
+                for (int64_t i = 0; i <= p->nv; i++) row_off[p->v_lo + i] = base + off[(size_t)i];
+            base += off[(size_t)p->nv];
+        }
+        return BFSX_OK;
+    }
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     if (g->d_perm) return export_csr_original(g->ctx->stream, g->nv, g->nnz, g->d_row_off, g->d_col, g->d_perm,
                                               g->d_inv, row_off, col);
@@ -762,8 +996,23 @@ int bfsx_graph_csr(const bfsx_graph *g, int64_t *row_off, uint32_t *col) {
     return BFSX_OK;
 }
 
+static int sample_roots_impl(bfsx_graph *g, int count, uint64_t seed, int64_t *roots);
+
 int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
     if (!g || !roots || count < 0) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) {
+        const int P = (int)g->parts.size();
+        std::vector<std::vector<int64_t>> got(P, std::vector<int64_t>((size_t)count + 1));
+        if (int rc = run_ranks(g->ctx->ranks, [&](int r) { return bfsx_sample_roots(g->parts[r], count, seed, got[r].data()); }))
+            return rc;
+        std::copy(got[0].begin(), got[0].begin() + count, roots);
+        return BFSX_OK;
+    }
+    const int rc = sample_roots_impl(g, count, seed, roots);
+    return g->nranks > 1 ? comm_guard(g->ctx->comm.get(), rc) : rc; // collective on a partition
+}
+
+static int sample_roots_impl(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
     // a partitioned graph samples collectively: the owner of each candidate decides, the verdict is
     // all-reduced, so every rank returns the same roots as the single-device graph would
     const bool part = g->nranks > 1;
@@ -803,7 +1052,7 @@ int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
             BFSX_HIP_TRY(hipMemcpyAsync(flag.p, &ok, sizeof(ok), hipMemcpyHostToDevice, st));
             if (int e = cm->allreduce_sum(flag.p, 1, st)) return e;
             BFSX_HIP_TRY(hipMemcpyAsync(&ok, flag.p, sizeof(ok), hipMemcpyDeviceToHost, st));
-            BFSX_HIP_TRY(hipStreamSynchronize(st));
+            if (int e = comm_sync(cm, st, "root sampling")) return e;
         }
         if (!ok) continue;
         seen.insert(x);
@@ -815,6 +1064,7 @@ int bfsx_sample_roots(bfsx_graph *g, int count, uint64_t seed, int64_t *roots) {
 
 int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_out, bfsx_stats *stats) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (is_group(g)) return group_bfs(g, source, dist_out, parent_out, stats);
     if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: run it with bfsx_dist_bfs (collective over the ranks)");
     const auto t0 = std::chrono::steady_clock::now();
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
@@ -844,6 +1094,20 @@ int bfsx_bfs(bfsx_graph *g, int64_t source, int32_t *dist_out, int64_t *parent_o
 int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first_bad, int64_t *reached,
                   int64_t *entries) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (is_group(g)) {
+        if (source < 0) source = g->last_source;
+        const int P = (int)g->parts.size();
+        std::vector<std::array<int64_t, 4>> res(P);
+        if (int rc = run_ranks(g->ctx->ranks, [&](int r) {
+                return bfsx_validate(g->parts[r], source, &res[r][0], &res[r][1], &res[r][2], &res[r][3]);
+            }))
+            return rc;
+        if (errors) *errors = res[0][0]; // collective: every rank holds the all-reduced verdict
+        if (first_bad) *first_bad = res[0][1];
+        if (reached) *reached = res[0][2];
+        if (entries) *entries = res[0][3];
+        return BFSX_OK;
+    }
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     int64_t res[4] = {0, -1, 0, 0};
     int64_t si = source;
@@ -854,7 +1118,7 @@ int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first
         if (source >= g->nv_global) return fail(BFSX_E_ARG, "source out of range");
         if (int rc = dist_map_source(g, source, &si)) return rc;
     }
-    if (int rc = bfs_validate(g, si, nullptr, res)) return rc;
+    if (int rc = bfs_validate(g, si, nullptr, res)) return g->nranks > 1 ? comm_guard(g->ctx->comm.get(), rc) : rc;
     if (int rc = to_original(g, res[1], &res[1])) return rc;
     if (errors) *errors = res[0];
     if (first_bad) *first_bad = res[1];
@@ -866,7 +1130,7 @@ int bfsx_validate(bfsx_graph *g, int64_t source, int64_t *errors, int64_t *first
 int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, const int64_t *parent, int64_t *errors,
                          int64_t *first_bad) {
     if (!g || !dist || !parent) return fail(BFSX_E_ARG, "null argument");
-    if (g->nranks > 1) return fail(BFSX_E_ARG, "partitioned graph: use bfsx_validate (collective)");
+    if (g->nranks > 1 || is_group(g)) return fail(BFSX_E_ARG, "partitioned graph: use bfsx_validate (collective)");
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     std::vector<unsigned long long> packed((size_t)g->nv);
     std::vector<uint32_t> perm;
@@ -904,12 +1168,26 @@ int bfsx_validate_result(bfsx_graph *g, int64_t source, const int32_t *dist, con
 
 int bfsx_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     if (!g) return fail(BFSX_E_ARG, "null graph");
+    if (is_group(g))
+        return run_ranks(g->ctx->ranks, [&](int r) {
+            bfsx_graph *p = g->parts[r];
+            return bfs_copy_result(p, dist_out ? dist_out + p->v_lo : nullptr, parent_out ? parent_out + p->v_lo : nullptr);
+        });
     BFSX_HIP_TRY(hipSetDevice(g->ctx->device));
     return bfs_copy_result(g, dist_out, parent_out);
 }
 
 int bfsx_level_times(bfsx_graph *g, double *cum_ms, int cap) {
     if (!g || (!cum_ms && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) { // per level: the slowest rank's cumulative device time
+        const int n = (int)std::min<size_t>(g->parts[0]->level_cum_ms.size(), (size_t)std::max(cap, 0));
+        for (int i = 0; i < n; i++) {
+            cum_ms[i] = 0;
+            for (const bfsx_graph *p : g->parts)
+                if ((size_t)i < p->level_cum_ms.size()) cum_ms[i] = std::max(cum_ms[i], p->level_cum_ms[i]);
+        }
+        return n;
+    }
     int n = (int)std::min<size_t>(g->level_cum_ms.size(), (size_t)std::max(cap, 0));
     for (int i = 0; i < n; i++) cum_ms[i] = g->level_cum_ms[i];
     return n;
@@ -930,12 +1208,18 @@ int bfsx_persist_fallbacks(const bfsx_graph *g, int64_t *count) {
 
 int bfsx_last_unpack_ms(const bfsx_graph *g, double *ms) {
     if (!g || !ms) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) {
+        *ms = -1.0;
+        for (const bfsx_graph *p : g->parts) *ms = std::max(*ms, bfs_last_unpack_ms(p));
+        return BFSX_OK;
+    }
     *ms = bfs_last_unpack_ms(g);
     return BFSX_OK;
 }
 
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap) {
     if (!g || (!dirs && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) return bfsx_level_dirs(g->parts[0], dirs, cap); // all-reduced: the same on every rank
     int n = (int)std::min<size_t>(g->level_dirs.size(), (size_t)std::max(cap, 0));
     for (int i = 0; i < n; i++) dirs[i] = g->level_dirs[i];
     return n;
@@ -943,6 +1227,26 @@ int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap) {
 
 int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap) {
     if (!g || (!out && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) { // counts summed over the ranks, times the slowest rank's
+        const int n = bfsx_level_stats(g->parts[0], out, cap);
+        std::vector<bfsx_level_stat> o((size_t)std::max(n, 1));
+        for (size_t q = 1; q < g->parts.size(); q++) {
+            const int k = std::min(n, bfsx_level_stats(g->parts[q], o.data(), n));
+            for (int i = 0; i < k; i++) {
+                out[i].frontier_in += o[i].frontier_in;
+                out[i].frontier_out += o[i].frontier_out;
+                out[i].mf_in += o[i].mf_in;
+                out[i].unvisited_in += o[i].unvisited_in;
+                out[i].scanned += o[i].scanned;
+                out[i].claims += o[i].claims;
+                out[i].stage2 += o[i].stage2;
+                out[i].walked += o[i].walked;
+                out[i].kernel_ms = std::max(out[i].kernel_ms, o[i].kernel_ms);
+                out[i].cum_ms = std::max(out[i].cum_ms, o[i].cum_ms);
+            }
+        }
+        return n;
+    }
     int n = (int)std::min<size_t>(g->level_stats.size(), (size_t)std::max(cap, 0));
     for (int i = 0; i < n; i++) out[i] = g->level_stats[i];
     return n;
@@ -950,6 +1254,9 @@ int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap) {
 
 int bfsx_device_synchronize(bfsx_ctx *ctx) {
     if (!ctx) return fail(BFSX_E_ARG, "null ctx");
+    for (bfsx_ctx *c : ctx->ranks)
+        if (int rc = bfsx_device_synchronize(c)) return rc;
+    if (is_group(ctx)) return BFSX_OK;
     BFSX_HIP_TRY(hipSetDevice(ctx->device));
     BFSX_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return BFSX_OK;

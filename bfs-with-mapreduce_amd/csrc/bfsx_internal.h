@@ -16,6 +16,7 @@ namespace bfsx {
 
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
+const std::string &last_error(); // the calling thread's message (bfsx_last_error)
 
 #define BFSX_STR2(x) #x
 #define BFSX_STR(x) BFSX_STR2(x)
@@ -64,12 +65,29 @@ struct Options {
     int test_overread = -1;     // test hook: that top-down level's kernels read one queue entry past the tail
     bool check_retired = false; // test hook: the partitioned loop fails if a launch or exchange uses a retired buffer
     int sparse_exchange = 1;    // partitioned pull levels: small global frontiers exchanged as id lists (0 off, 1 auto, 2 on)
+    int64_t comm_timeout_ms = 120000; // partitioned path: a host wait on the peers fails after this long
+    bool check_collectives = false;   // debug: every collective checks that all ranks are in the same (op, level)
+    int fail_rank = -1, fail_level = -1; // test hook (fault injection): that rank fails at that level of the loop
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------
 // Stream-ordered collectives on device buffers (RCCL, or an in-process group of host threads).
+//
+// Failure handling ("A failed rank fails every rank"): a collective loop is only as live as its
+// slowest rank, so a rank that leaves a collective call with an error calls abort() (comm_guard below), which
+// makes every peer's pending and later collectives fail with BFSX_E_RCCL "peer rank r failed ...": the
+// in-process group wakes its waiters; RCCL ranks signal each other through a node-local shared-memory board
+// and ncclCommAbort their communicators.  Every host wait of the partitioned path polls for that (poll(), from
+// post_wait and comm_sync) and gives up after `timeout_ms` (a rank that died or diverged without signalling).
+// An aborted communicator stays failed, like an aborted NCCL communicator.
+enum CommOp : int { kOpAllreduce = 1, kOpAlltoall1 = 2, kOpAlltoallv = 3, kOpAllgather = 4 };
+const char *comm_op_name(int op);
 struct Comm {
     int rank = 0, nranks = 1;
+    int tag = -1;                // the partitioned loop's level (-1: setup, -2: after the loop): names a collective
+    int64_t timeout_ms = 120000; // option comm_timeout_ms: a host wait on the peers fails after this long
+    bool check_seq = false;      // option check_collectives: every collective compares (op, level) across the ranks
+    bool agreed = false;         // the error being returned was reached by every rank at the same point: no abort
     virtual ~Comm() = default;
     virtual int allreduce_sum(int64_t *d_buf, int n, hipStream_t st) = 0;              // in place
     // one value per rank; d_recv[rank] (the value a rank sends itself) may be left unwritten
@@ -77,7 +95,24 @@ struct Comm {
     virtual int alltoallv(const unsigned long long *d_send, const int64_t *scount, const int64_t *sdispl, unsigned long long *d_recv,
                           const int64_t *rcount, const int64_t *rdispl, hipStream_t st) = 0; // host counts
     virtual int allgather(const unsigned long long *d_in, int64_t n, unsigned long long *d_out, hipStream_t st) = 0;
+    // This rank failed with (code, msg): every peer's pending and later collectives fail.  Idempotent; a no-op
+    // when a peer's abort is what failed this rank.
+    virtual void abort(int code, const std::string &msg) = 0;
+    // Between spins of a host wait that started at t0_ns (steady clock): BFSX_OK, or BFSX_E_RCCL with the
+    // message set once any rank aborted or the wait outlived timeout_ms (which aborts the group).
+    virtual int poll(int64_t t0_ns, const char *what) = 0;
+    virtual bool failed() const = 0; // aborted (by this rank or a peer): every call fails
 };
+int64_t now_ns();
+// hipStreamSynchronize for the partitioned path: polls the communicator while the stream drains
+int comm_sync(Comm *cm, hipStream_t st, const char *what);
+// After a collective entry point returned rc on this rank: abort the group when rc is this rank's own error
+// (not a peer's abort it merely observed), so no peer waits for it.  Returns rc.
+int comm_guard(Comm *cm, int rc);
+void comm_sync_options(bfsx_ctx *ctx); // the context's comm_timeout_ms / check_collectives onto its communicator
+// ranks ctxs[0..n) of one process, one host thread each: an RCCL clique over their (distinct) devices, or the
+// in-process group (rccl = false)
+int comm_clique(bfsx_ctx **ctxs, int nranks, bool rccl);
 
 // ---- kernels_build.hip -------------------------------------------------------------------
 // Builds the CSR (sorted, de-duplicated neighbour sets, self-loops kept once) from device tuple
@@ -149,6 +184,9 @@ struct bfsx_ctx {
     bfsx::Options opt;
     int num_cus = 256;
     std::unique_ptr<bfsx::Comm> comm; // partitioned path: set by bfsx_comm_init / bfsx_comm_local_group
+    // a group context (bfsx_init_group): one rank context per rank, driven by one host thread each inside every
+    // call on the group; the group itself holds no stream or communicator
+    std::vector<bfsx_ctx *> ranks;
 };
 
 struct bfsx_graph {
@@ -165,6 +203,9 @@ struct bfsx_graph {
     // internal id; perm[original] = internal, inv[internal] = original.  Null: internal = original.
     uint32_t *d_perm = nullptr, *d_inv = nullptr;
     bfsx::BfsWorkspace *ws = nullptr;
+    // a graph of a group context: rank r's partition (rows of global ids [r*chunk, ...)) in parts[r]; the group
+    // graph's own fields hold nv_global / nnz (sum) / m and nothing is on a device under it directly
+    std::vector<bfsx_graph *> parts;
     // host memo of the immutable per-source lookups a BFS start reads back from the device (each a synchronous
     // 4-16 B copy, ~10 us of host time): original -> internal id, internal id -> its row bounds.  Bounded.
     std::unordered_map<int64_t, int64_t> perm_memo;

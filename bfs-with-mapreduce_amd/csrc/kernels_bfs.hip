@@ -1346,10 +1346,14 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 //   (bottom-up): either tells the next push level whether it needs the hub bin.
 //   out[11 + r], r < nranks: this rank's n_f in its own slot, 0 elsewhere -- all-reduced with out[8..10], every
 //   rank learns every rank's frontier size (the sparse frontier exchange's receive counts).
+//   out[11 + nranks]: bit `rank` set when this rank's queue guard (id_ok, `err`) has fired -- all-reduced too, so
+//   every rank leaves the loop at the same level with the same error instead of the failing rank alone (the
+//   guard used to be read only after the loop, between the last level close and the m_comp all-reduce: a
+//   rank-local early return that left its peers inside that all-reduce, DESIGN.md 4, event (c)).
 // One wave (threads 0..63) of the calling workgroup; the shards are read with agent-scope loads, so a
 // last-arriving workgroup of the level's last kernel can run it (k_claim_remote) as well as k_level_sums.
 __device__ inline void level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
-                                  u64 *__restrict__ ctr, int nctr, int rank, int nranks) {
+                                  u64 *__restrict__ ctr, int nctr, int rank, int nranks, const u64 *err) {
     if (threadIdx.x >= 64) return;
     const unsigned lane = threadIdx.x;
     auto ld = [](const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1371,6 +1375,8 @@ __device__ inline void level_sums(const LevelSlot *__restrict__ slot, int topdow
         for (int i = 0; i < 3; i++) out[8 + i] = (int64_t)t[i];
         out[7] = (int64_t)(topdown ? dmax : nhub);
         for (int r = 0; r < nranks; r++) out[11 + r] = r == rank ? (int64_t)t[0] : 0;
+        const u64 e = err ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+        out[11 + nranks] = e ? (int64_t)(1ull << rank) : 0; // distinct bits: the all-reduced sum is their OR
     }
 }
 // Multi-GPU: claim the (v, parent) pairs other ranks routed to this rank's vertices.
@@ -1426,18 +1432,23 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     if (threadIdx.x == 0)
         s_last = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
     __syncthreads();
-    if (s_last) level_sums(cn, 1, sums, ctr, nctr, rank, nranks);
+    if (s_last) level_sums(cn, 1, sums, ctr, nctr, rank, nranks, err);
 }
 
 // Multi-GPU: stable bucketing of remote pairs by owning rank (P <= kMaxRanks).  Two passes over the
 // pairs: per-workgroup destination histograms (LDS atomics), then one reservation atomic per
 // (workgroup, destination) and LDS-ranked scatter.
-// multi-GPU counter block: [0] remote tail | count[64] | cursor[64] | arrivals | recv count[64] | level sums[16]
+// multi-GPU counter block: [0] remote tail | count[64] | cursor[64] | arrivals | recv count[64] | level sums[16 + 64]
 constexpr int kCtrHead = 2 + 2 * kMaxRanks; // zeroed per level (the last word: k_claim_remote's arrivals)
 constexpr int kCtrRecv = kCtrHead;
 constexpr int kCtrSums = kCtrHead + kMaxRanks;
-constexpr int kCtrSums16 = 16 + kMaxRanks; // level sums: [0..10] as level_sums writes them, [11, 11 + P) per-rank n_f
+// level sums: [0..10] as level_sums writes them, [11, 11 + P) per-rank n_f, [11 + P] the ranks whose queue guard fired
+constexpr int kCtrSums16 = 16 + kMaxRanks;
 constexpr int kCtrWords = kCtrSums + kCtrSums16;
+constexpr int kPostWords = 1 + 2 * kMaxRanks + 16; // mapped host words of k_post: sequence + posted values
+static_assert(12 + kMaxRanks <= kCtrSums16, "level sums overrun their block");
+static_assert(12 + kMaxRanks <= kPostWords - 1, "a level close posts 12 + P words");
+static_assert(2 * kMaxRanks <= kPostWords - 1, "a count exchange posts 2P words");
 
 
 __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
@@ -2462,8 +2473,8 @@ __global__ void k_post(const u64 *__restrict__ a, int na, const u64 *__restrict_
 // (the copy is all-reduced in place; the local half stays for the per-level record), and zeroes the
 // next top-down level's exchange counters `ctr` (nothing reads them after this level's claim kernel).
 __global__ void k_level_sums(const LevelSlot *__restrict__ slot, int topdown, int64_t *__restrict__ out,
-                             u64 *__restrict__ ctr, int nctr, int rank, int nranks) {
-    level_sums(slot, topdown, out, ctr, nctr, rank, nranks);
+                             u64 *__restrict__ ctr, int nctr, int rank, int nranks, const u64 *err) {
+    level_sums(slot, topdown, out, ctr, nctr, rank, nranks, err);
 }
 
 unsigned clamp_grid(int64_t blocks, unsigned cap) {
@@ -2899,12 +2910,19 @@ int wait_published(BfsWorkspace *ws, hipStream_t st) {
     return BFSX_OK;
 }
 
-// Post `na` words at a and `nb` at b to the host (in order) and wait for them; out gets na + nb words.
-int post_wait(BfsWorkspace *ws, hipStream_t st, const u64 *a, int na, const u64 *b, int nb, u64 *out) {
+// Post `na` words at a and `nb` at b to the host (in order) and wait for them; out gets na + nb words.  The
+// partitioned loop passes its communicator: the wait then also ends (BFSX_E_RCCL) when a peer rank aborted or
+// the wait outlived the communicator's deadline (Comm::poll), instead of spinning behind a collective that
+// will never complete.
+int post_wait(BfsWorkspace *ws, hipStream_t st, const u64 *a, int na, const u64 *b, int nb, u64 *out,
+              Comm *cm = nullptr, const char *what = "a level close") {
     hipLaunchKernelGGL(k_post, dim3(1), dim3(64), 0, st, a, na, b, nb, ws->d_post, ++ws->post_seq);
     BFSX_LAUNCHED(st);
     const volatile u64 *seq = ws->h_post;
+    const int64_t t0 = cm ? now_ns() : 0;
     for (uint64_t spin = 1; *seq != ws->post_seq; spin++) {
+        if (cm && (spin & 0xFFF) == 0)
+            if (int rc = cm->poll(t0, what)) return rc;
         if ((spin & 0xFFFF) == 0) {
             const hipError_t e = hipStreamQuery(st);
             if (e != hipSuccess && e != hipErrorNotReady)
@@ -3814,7 +3832,7 @@ int dist_ws(bfsx_graph *g) {
     if (rc) return rc;
     if (!g->ws->d_dist_ctr) BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, kCtrWords * sizeof(u64)));
     if (!g->ws->h_post) {
-        BFSX_HIP_TRY(hipHostMalloc(&g->ws->h_post, (1 + 2 * kMaxRanks + 16) * sizeof(u64),
+        BFSX_HIP_TRY(hipHostMalloc(&g->ws->h_post, kPostWords * sizeof(u64),
                                    hipHostMallocMapped | hipHostMallocCoherent));
         BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&g->ws->d_post, g->ws->h_post, 0));
         g->ws->h_post[0] = 0;
@@ -3869,7 +3887,14 @@ int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_kn
                        ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_LAUNCHED(st);
     ws->prev_source = sl;
-    ws->n_prec = 0; // the partitioned loop stores packed states only (no pull-level records)
+    // no pull-level records and no push log yet: the level primitives (tests/dist_driver.py) store packed states
+    // only, and the native loop (dist_bfs_run) keeps its pull levels' records through its own RecLog.  A push log
+    // left pending by an earlier one-device BFS on this workspace must not be scattered over this result.
+    ws->n_prec = 0;
+    ws->log_n = 0;
+    ws->log_end.clear();
+    ws->log_nd.clear();
+    ws->logs_pending = false;
     ws->resolved = true;
     ws->d_level = 0;
     ws->d_dir = BFSX_DIR_TOPDOWN;
@@ -4083,7 +4108,7 @@ void trace_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level) {
              {"rest", ws->rest, nv * 16},                {"ring", ws->ring, 3 * (int64_t)sizeof(LevelSlot)},
              {"remote", ws->remote, ws->remote_cap * 8}, {"sendbuf", ws->sendbuf, ws->send_cap * 8},
              {"recvbuf", ws->recvbuf, ws->recv_cap * 8}, {"fglob", ws->fglob, ws->fglob_words * 8},
-             {"dist_ctr", ws->d_dist_ctr, kCtrWords * 8}, {"post", ws->d_post, (1 + 2 * kMaxRanks + 16) * 8},
+             {"dist_ctr", ws->d_dist_ctr, kCtrWords * 8}, {"post", ws->d_post, kPostWords * 8},
              {"err", ws->d_err, 8},                      {"pub", ws->d_pub, (int64_t)sizeof(Published)}};
     for (const auto &x : b)
         fprintf(stderr, "[bfsx] rank %d level %d buffer %-8s [0x%llx, 0x%llx)\n", g->rank, level, x.name,
@@ -4161,7 +4186,7 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
     if (int e = cm->allgather(b.cnt, 1, b.cnt + 1, st)) return e;
     std::vector<u64> counts(P, 0);
     BFSX_HIP_TRY(hipMemcpyAsync(counts.data(), b.cnt + 1, P * sizeof(u64), hipMemcpyDeviceToHost, st));
-    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    if (int e = comm_sync(cm, st, "the degree-list all-gather")) return e;
     u64 maxc = 0;
     bool over = false;
     for (int p = 0; p < P; p++) {
@@ -4182,7 +4207,7 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
         if (int e = cm->allgather(b.sel, (int64_t)maxc, b.all, st)) return e;
         std::vector<u64> h(P * maxc);
         BFSX_HIP_TRY(hipMemcpyAsync(h.data(), b.all, h.size() * sizeof(u64), hipMemcpyDeviceToHost, st));
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        if (int e = comm_sync(cm, st, "the degree-list all-gather")) return e;
         for (u64 x : h)
             if (x != ~0ull) ws->h_big.push_back(x);
         std::sort(ws->h_big.begin(), ws->h_big.end());
@@ -4198,13 +4223,14 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[kCtrS
     int64_t *sums = reinterpret_cast<int64_t *>(ws->d_dist_ctr + kCtrSums);
     if (!summed) {
         hipLaunchKernelGGL(k_level_sums, dim3(1), dim3(64), 0, st, ws->ring + (level + 1) % 3, td ? 1 : 0, sums,
-                           ws->d_dist_ctr, kCtrHead, g->rank, g->nranks);
+                           ws->d_dist_ctr, kCtrHead, g->rank, g->nranks, ws->d_err);
         BFSX_LAUNCHED(st);
     }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
-    if (int e = g->ctx->comm->allreduce_sum(sums + 8, 3 + g->nranks, st)) return e;
-    return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 11 + g->nranks, nullptr, 0,
-                     reinterpret_cast<u64 *>(out));
+    Comm *cm = g->ctx->comm.get();
+    if (int e = cm->allreduce_sum(sums + 8, 4 + g->nranks, st)) return e;
+    return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 12 + g->nranks, nullptr, 0,
+                     reinterpret_cast<u64 *>(out), cm, "a level close");
 }
 
 // Option sparse_exchange: a pull level's global frontier travels as an id list when it holds fewer than n/128
@@ -4216,13 +4242,10 @@ bool sparse_exchange(const bfsx_graph *g, int64_t nf_global, const std::vector<i
     return mode == 2 || nf_global * 128 < g->nv_global;
 }
 
-} // namespace
-
-int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
-    Comm *cm = g->ctx->comm.get();
-    if (!cm) return fail(BFSX_E_ARG, "no communicator on this context (bfsx_comm_init / bfsx_comm_local_group)");
-    if (cm->nranks != g->nranks || cm->rank != g->rank)
-        return fail(BFSX_E_ARG, "graph partition does not match the communicator's rank/size");
+int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
+    cm->tag = -1;
+    if (g->ctx->opt.fail_rank == g->rank && g->ctx->opt.fail_level == -2) // test hook: before any collective
+        return fail(BFSX_E_HIP, "fault injection: rank " + std::to_string(g->rank) + " fails before the first collective");
     int rc = dist_ws(g);
     if (rc) return rc;
     BfsWorkspace *ws = g->ws;
@@ -4239,7 +4262,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, sizeof(int64_t), hipMemcpyHostToDevice, st));
         if (int e = cm->allreduce_sum(sums + 8, 1, st)) return e;
         BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        if (int e = comm_sync(cm, st, "the adjacency-count all-reduce")) return e;
         ws->nnz_global = h[0];
     }
     if (ws->big_thr < 0) {
@@ -4261,12 +4284,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     }
     int64_t deg_local = 0;
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st)); // before the timed region
-    // the partitioned loop keeps the packed-state stores (no push log): a stale log of an earlier one-device BFS
-    // on this workspace must not be applied to this result
-    ws->log_n = 0;
-    ws->log_end.clear();
-    ws->log_nd.clear();
-    ws->logs_pending = false;
+    // (dist_begin clears a stale push log of an earlier one-device BFS on this workspace)
     if ((rc = dist_begin(g, source, &deg_local, deg))) return rc;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
@@ -4297,6 +4315,10 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
     std::vector<u64> hc(2 * kMaxRanks);
     for (;;) {
         const int level = ws->d_level;
+        cm->tag = level;
+        if (opt.fail_rank == g->rank && opt.fail_level == level) // test hook: this rank fails mid-BFS
+            return fail(BFSX_E_HIP, "fault injection: rank " + std::to_string(g->rank) + " fails at level " +
+                                        std::to_string(level));
         if (opt.direction == BFSX_DIR_AUTO && level > 0) {
             // Beamer's rule, plus the exchange cost: a top-down level ships up to 8*m_f*(P-1)/P bytes of
             // (vertex, parent) pairs, a bottom-up level all-gathers an n/8-byte bitmap -- pull as soon as
@@ -4388,7 +4410,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
                 u64 *drecv = ws->d_dist_ctr + kCtrRecv;
                 if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
                     return e;
-                if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data())) return e;
+                if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data(), cm, "a pair-count exchange")) return e;
                 hc[P + g->rank] = 0; // alltoall1 does not exchange the own entry (no pairs route to it)
                 plan_counted(P, hc.data(), hc.data() + P, plan);
                 ro = plan.recv_total;
@@ -4487,6 +4509,15 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
             bu_levels++;
         }
         if (int e = dist_level_close(g, ws, td, h, summed)) return e;
+        if (h[11 + P] != 0) { // a queue guard fired on some rank(s) this level: every rank fails here, together
+            std::string who;
+            for (int r = 0; r < P; r++)
+                if ((uint64_t)h[11 + P] >> r & 1ull) who += (who.empty() ? "" : ", ") + std::to_string(r);
+            std::string mine;
+            if (check_queue_guard(ws)) mine = " (this rank: " + last_error() + ")";
+            cm->agreed = true; // every rank leaves here with this error: the communicator stays usable
+            return fail(BFSX_E_HIP, "queue guard fired at level " + std::to_string(level) + " on rank(s) " + who + mine);
+        }
         static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
         if (trace)
             fprintf(stderr, "[bfsx] rank %d level %d %s: nf %lld -> %lld (global %lld)\n", g->rank, level,
@@ -4530,6 +4561,7 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         }
         if (nf == 0) break;
     }
+    cm->tag = -2;
     recs.finish();
     if ((rc = dist_finish(g))) return rc;
     if (stats) {
@@ -4548,11 +4580,27 @@ int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
         BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, 2 * sizeof(int64_t), hipMemcpyHostToDevice, st));
         if (int e = cm->allreduce_sum(sums + 8, 2, st)) return e;
         BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        if (int e = comm_sync(cm, st, "the m_comp all-reduce")) return e;
         stats->m_comp = h[0];
         stats->reached = h[1];
     }
     return BFSX_OK;
+}
+
+} // namespace
+
+// The partitioned BFS, collective: a rank that fails aborts the group (comm_guard), so every rank returns an
+// error instead of waiting for it inside a collective ("A failed rank fails every rank").
+int dist_bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats) {
+    Comm *cm = g->ctx->comm.get();
+    if (!cm) return fail(BFSX_E_ARG, "no communicator on this context (bfsx_comm_init / bfsx_comm_local_group)");
+    if (cm->nranks != g->nranks || cm->rank != g->rank)
+        return fail(BFSX_E_ARG, "graph partition does not match the communicator's rank/size");
+    if (cm->failed()) return cm->poll(now_ns(), "a BFS on an aborted communicator");
+    // argument errors are the same on every rank (every rank passes the same source): no abort
+    if (source < 0 || source >= g->nv_global) return fail(BFSX_E_RANGE, "source vertex outside the graph");
+    comm_sync_options(g->ctx);
+    return comm_guard(cm, dist_bfs_impl(g, source, stats, cm));
 }
 
 } // namespace bfsx

@@ -7,6 +7,9 @@
 //     (ServiceConfiguration.java:30-43): app-name, ip, port, jar, problemFiles (comma-separated,
 //     Splitter.on(",") -- no trimming).  Optional keys added here, defaults = reference behaviour:
 //       source=0 (GraphFileUtil.java:28)  device=0  direction=auto|topdown|bottomup
+//       devices=1 (N > 1: one call runs N ranks of a 1-D vertex partition inside this process, bfsx_init_group --
+//         an RCCL clique over N GPUs, or an in-process group when fewer GPUs are visible; the Spark workers of
+//         the reference's cluster, BfsSpark.java:44,50)
 //       writeInitial=true (problemFile_0, GraphFileUtil.java:68)  writePaths=true
 //       dumpLevels=false (every intermediate problemFile_<k>, BfsSpark.java:115-116)
 //       validate=false (Graph500-style check of the result on the device, bfsx_validate; logged)
@@ -401,10 +404,22 @@ int main(int argc, char **argv) {
         log_line("INFO", "main", 46, "Problem files path: " + lst + "]");
     }
     log_line("INFO", "main", 47, "Using JAR file: " + get("jar", ""));
-    log_line("INFO", "main", 48, "Connecting to: " + master + " (replaced by libbfsx on HIP device " +
-                                     get("device", "0") + ")");
+    const int devices = std::atoi(get("devices", "1").c_str());
+    if (devices < 1 || devices > 64) {
+        std::fprintf(stderr, "devices must be in [1, 64]\n");
+        return 2;
+    }
     bfsx_ctx *ctx = nullptr;
-    int rc = bfsx_init(std::atoi(get("device", "0").c_str()), &ctx);
+    int rc = BFSX_OK;
+    if (devices == 1) {
+        log_line("INFO", "main", 48, "Connecting to: " + master + " (replaced by libbfsx on HIP device " +
+                                         get("device", "0") + ")");
+        rc = bfsx_init(std::atoi(get("device", "0").c_str()), &ctx);
+    } else {
+        log_line("INFO", "main", 48, "Connecting to: " + master + " (replaced by libbfsx: " + std::to_string(devices) +
+                                         " ranks of a 1-D vertex partition, one per HIP device)");
+        rc = bfsx_init_group(devices, &ctx);
+    }
     if (rc) {
         std::fprintf(stderr, "bfsx_init failed: %s\n", bfsx_last_error());
         return 3;

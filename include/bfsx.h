@@ -91,6 +91,17 @@ int bfsx_abi_version(void);
 const char *bfsx_last_error(void);
 /* Replaces: new JavaSparkContext(...) + spark.addJar (BfsSpark.java:50-51). device = HIP ordinal. */
 int bfsx_init(int device, bfsx_ctx **out);
+/* A group context: nranks ranks inside this process, rank r on HIP device r % (visible devices), one host thread
+ * per rank inside every call.  Replaces the Spark cluster the reference connects to (BfsSpark.java:44,50): every
+ * graph built on a group context is 1-D partitioned over its ranks (as bfsx_dist_graph_*), and bfsx_bfs /
+ * bfsx_result / bfsx_validate / bfsx_level_* on such a graph run the partitioned level loop on all ranks and
+ * return once, with whole-graph outputs -- the caller sees one call.  The exchange is an RCCL
+ * clique over xGMI when the ranks have distinct devices (ncclCommInitAll), else (ranks sharing a device) the
+ * in-process group; environment BFSX_GROUP_COMM=local|rccl forces one.  bfsx_set_option applies to every rank.
+ * Not available on a group graph: bfsx_validate_result, the bfsx_dist_* calls, bfsx_comm_*. */
+int bfsx_init_group(int nranks, bfsx_ctx **out);
+/* Ranks of a context: 1 for a bfsx_init context. */
+int bfsx_group_size(const bfsx_ctx *ctx);
 void bfsx_finalize(bfsx_ctx *ctx);
 /* Options (all optional; defaults preserve reference behaviour):
  *   "direction" = auto|topdown|bottomup ; "alpha" = int (default 20) ; "beta" = int (default 24)
@@ -147,7 +158,14 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 all-gather (auto, the default); on: every pull level at P > 1; off: never)
  *   "big_degree", "big_cap" = int (partitioned graphs: the ids of degree > big_degree, at most big_cap per
  *                 rank, are all-gathered with their degrees at the first BFS, so every rank knows a source's
- *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS) */
+ *                 degree; defaults 4096 and 2^20; read at a graph's first partitioned BFS)
+ *   "comm_timeout_ms" = int (partitioned graphs: a host wait on the other ranks fails with BFSX_E_RCCL after this
+ *                 long and aborts the communicator; 0 = no deadline; default 120000.  A rank that FAILS aborts
+ *                 the communicator at once: every rank's call then returns BFSX_E_RCCL "peer rank r failed ...")
+ *   "check_collectives" = on|off (debug: every collective first checks that all ranks are in the same
+ *                 collective of the same level, and fails on every rank with both names otherwise)
+ *   "fail_at" = rank:level|rank:setup|off (test hook: that rank of a partitioned BFS fails at the start of that
+ *                 level, or before its first collective) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */
@@ -246,12 +264,16 @@ int bfsx_dist_graph_from_edges(bfsx_ctx *ctx, int64_t nv, const uint32_t *u, con
                                int rank, int nranks, bfsx_graph **out);
 int bfsx_dist_graph_kronecker(bfsx_ctx *ctx, int scale, int edgefactor, uint64_t seed, int rank, int nranks,
                               bfsx_graph **out);
+/* GraphFileUtil.convert (GraphFileUtil.java:45-69) for one rank of a partition: the rank tokenizes the whole
+ * algs4 file on its own GPU and keeps the rows of the ids it owns (same errors as bfsx_graph_load_algs4). */
+int bfsx_dist_graph_load_algs4(bfsx_ctx *ctx, const char *path, int rank, int nranks, bfsx_graph **out);
 int bfsx_graph_partition(const bfsx_graph *g, int64_t *nv_global, int64_t *v_lo, int64_t *nv_local,
                          int64_t *chunk, int32_t *rank, int32_t *nranks);
 /* Degree of global id v if this rank owns it (else -1). */
 int bfsx_graph_degree(const bfsx_graph *g, int64_t v, int64_t *deg);
 
 /* ---- multi-GPU, native exchange: the whole partitioned level loop inside the library ------------
+ * (For N ranks inside ONE process, bfsx_init_group does all of the below for the caller.)
  * One rank per GPU.  The exchange runs over RCCL (xGMI) on the BFS stream: top-down levels route
  * (vertex, parent) pairs to their owners (all-to-all of counts + grouped send/recv), bottom-up levels
  * all-gather the frontier bitmap slices, every level all-reduces (n_f, m_f, m_u).
@@ -260,7 +282,10 @@ int bfsx_graph_degree(const bfsx_graph *g, int64_t v, int64_t *deg);
  * bfsx_comm_local_group: the same exchange for nranks contexts inside ONE process (one host thread
  * per rank; ranks may share a device) -- the partitioned path testable on a single GPU.
  * bfsx_dist_bfs: collective; every rank passes the same source.  Results: bfsx_result (local rows).
- * stats, if requested, must be requested by every rank (m_comp/reached are all-reduced). */
+ * stats, if requested, must be requested by every rank (m_comp/reached are all-reduced).
+ * Failure: every collective call (bfsx_dist_bfs, bfsx_sample_roots and bfsx_validate on a partition) that fails on
+ * one rank aborts the communicator, so it fails on every rank (BFSX_E_RCCL naming the failed rank and its level)
+ * instead of leaving the others inside a collective; an aborted communicator fails every later call. */
 #define BFSX_COMM_ID_BYTES 128
 int bfsx_comm_unique_id(uint8_t *id);
 int bfsx_comm_init(bfsx_ctx *ctx, int rank, int nranks, const uint8_t *id);

@@ -32,6 +32,9 @@ def fake_bfsx():
         def dist_bfs(self, r, want_stats=True):
             if want_stats:  # all-reduced stats: identical on every rank; root 3 sits in a tiny component
                 return {"m_comp": 5 if r == 3 else self.m // 2}
+            if os.environ.get("BFSX_FAKE_HANG_RANK") == str(self.rank):  # a rank stuck in a collective
+                import time
+                time.sleep(3600)
             return 1.0 + 0.5 * self.rank + 0.01 * r  # device ms of this rank; rank world-1 is the slowest
 
         def validate(self, source=-1):

@@ -59,3 +59,22 @@ def test_bench_refuses_mismatched_world_size():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--scale", "12"], cwd=ROOT,
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and not r.stdout.strip(), (r.returncode, r.stdout, r.stderr[-2000:])
+
+
+def test_bench_deadline_ends_a_stuck_run():
+    """A rank stuck in the timed loop (here the stand-in's rank 1 never returns from its BFS, as a rank left inside
+    a collective by a failed peer would) must not hold the run past --deadline: every rank arms it, the stuck one
+    exits 124, torch.distributed.run stops the other, and `bench.py --gpus 2` exits non-zero with no JSON line,
+    long before the test's own limit."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", BFSX_FAKE_HANG_RANK="1",
+               BFSX_BENCH_BINDING=os.path.join(ROOT, "tests", "bench_dist_fake.py"))
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--scale", "12", "--roots",
+                        "4", "--steps", "2", "--warmup", "1", "--deadline", "20"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    took = time.time() - t0
+    assert r.returncode != 0 and not r.stdout.strip(), (r.returncode, r.stdout, r.stderr[-3000:])
+    assert "deadline of 20 s passed" in r.stderr, r.stderr[-3000:]
+    assert took < 150, took

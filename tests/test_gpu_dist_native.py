@@ -22,9 +22,27 @@ pytestmark = pytest.mark.gpu
 INF = 2147483647
 
 
+# Every group of this suite runs with the collective-sequence guard on (a rank in a different collective or level
+# fails every rank, naming both) and a 60 s deadline on every wait for a peer, so a hang becomes an error well
+# inside the test's own limit.
+GROUP_DEFAULTS = {"check_collectives": "on", "comm_timeout_ms": "60000"}
+
+
+def join_ranks(ths, errs, limit=90.0):
+    """Join the rank threads against one deadline; a thread still alive after it fails the test with every
+    rank's error so far (the errors of ranks that did return are the diagnosis of a hang)."""
+    import time
+    end = time.time() + limit
+    for t in ths:
+        t.join(timeout=max(0.0, end - time.time()))
+    alive = [i for i, t in enumerate(ths) if t.is_alive()]
+    assert not alive, f"rank thread(s) {alive} still inside the library after {limit} s; errors so far: {errs}"
+
+
 def run_group(bfsx, world, make_graph, sources, direction="auto", options=None):
     """One thread per rank; returns per source: (stats, dist, parent, dirs) assembled globally."""
-    ctxs = [bfsx.Context(0, direction=direction, **(options or {})) for _ in range(world)]
+    opts = dict(GROUP_DEFAULTS, **(options or {}))
+    ctxs = [bfsx.Context(0, direction=direction, **opts) for _ in range(world)]
     graphs = [None] * world
     try:
         bfsx.local_group(ctxs)
@@ -45,10 +63,8 @@ def run_group(bfsx, world, make_graph, sources, direction="auto", options=None):
             ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
             for t in ths:
                 t.start()
-            for t in ths:
-                t.join(timeout=120)
+            join_ranks(ths, errs)
             assert not errs, errs
-            assert all(not t.is_alive() for t in ths), "rank thread hung"
             nv = graphs[0].partition()["nv_global"]
             dist = np.full(nv, INF, np.int32)
             parent = np.full(nv, -1, np.int64)
@@ -328,3 +344,185 @@ def test_native_group_source_degrees(bfsx, options):
             g.free()
         for c in ctxs:
             c.close()
+
+
+def run_ranks_timed(ths):
+    import time
+    t0 = time.time()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=60)
+    return time.time() - t0
+
+
+@pytest.mark.parametrize("world,rank,where", [(2, 1, "2"), (2, 0, "0"), (4, 2, "1"), (4, 3, "3"), (4, 1, "setup"),
+                                              (2, 1, "setup")])
+def test_native_group_failed_rank_fails_every_rank(bfsx, world, rank, where):
+    """a rank that fails (fault injection, option fail_at=rank:level) aborts the group, so
+    EVERY rank's bfsx_dist_bfs returns an error within 5 s -- the failing rank its own, its peers BFSX_E_RCCL
+    "peer rank r failed at level k: ..." -- instead of waiting for it inside a collective forever (the round-4
+    record r04am: one rank left inside bfsx_dist_bfs, its peer gone).  The group stays failed afterwards, as an
+    aborted NCCL communicator does; a fresh group on the same contexts' graphs is not needed for that check."""
+    scale, seed = 13, 0xFA11
+    ctxs = [bfsx.Context(0, **dict(GROUP_DEFAULTS, fail_at=f"{rank}:{where}")) for _ in range(world)]
+    graphs = []
+    try:
+        bfsx.local_group(ctxs)
+        graphs = [ctxs[r].dist_kronecker(scale, r, world, seed=seed) for r in range(world)]
+        src = int(O.kronecker(scale, 16, seed)[0][0])
+        errs = [None] * world
+
+        def work(r):
+            try:
+                graphs[r].dist_bfs(src)
+            except bfsx.BfsxError as e:
+                errs[r] = (e.code, str(e))
+
+        ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        took = run_ranks_timed(ths)
+        assert all(not t.is_alive() for t in ths), f"rank thread hung after a peer failed: {errs}"
+        assert took < 5.0, took
+        assert all(e is not None for e in errs), errs
+        lvl = "setup" if where == "setup" else f"level {where}"
+        assert "fault injection" in errs[rank][1], errs
+        for r in range(world):
+            if r != rank:
+                assert errs[r][0] == bfsx.BFSX_E_RCCL, errs
+                assert f"peer rank {rank} failed at {lvl}" in errs[r][1] and "fault injection" in errs[r][1], errs
+        # the aborted group fails every later call at once, on every rank
+        errs2 = [None] * world
+
+        def again(r):
+            try:
+                graphs[r].dist_bfs(src)
+            except bfsx.BfsxError as e:
+                errs2[r] = str(e)
+
+        ths = [threading.Thread(target=again, args=(r,)) for r in range(world)]
+        assert run_ranks_timed(ths) < 5.0
+        assert all(e is not None and "fault injection" in e for e in errs2), errs2
+    finally:
+        for g in graphs:
+            g.free()
+        for c in ctxs:
+            c.close()
+
+
+def test_native_group_collective_mismatch_detected(bfsx):
+    """Option check_collectives: ranks in different collectives (here rank 0 validates while rank 1 starts the
+    next BFS) fail on every rank with both collectives named, instead of pairing one rank's all-gather with the
+    other's exchange."""
+    world, scale, seed = 2, 12, 0xC011
+    ctxs = [bfsx.Context(0, **GROUP_DEFAULTS) for _ in range(world)]
+    graphs = []
+    try:
+        bfsx.local_group(ctxs)
+        graphs = [ctxs[r].dist_kronecker(scale, r, world, seed=seed) for r in range(world)]
+        src = int(O.kronecker(scale, 16, seed)[0][0])
+        errs = [None] * world
+
+        def first(r):
+            graphs[r].dist_bfs(src)
+
+        ths = [threading.Thread(target=first, args=(r,)) for r in range(world)]
+        run_ranks_timed(ths)
+
+        def work(r):
+            try:
+                if r == 0:
+                    graphs[r].validate()
+                else:
+                    graphs[r].dist_bfs(src)
+            except bfsx.BfsxError as e:
+                errs[r] = str(e)
+
+        ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        assert run_ranks_timed(ths) < 5.0
+        assert all(e is not None for e in errs), errs
+        assert any("collective mismatch" in e for e in errs), errs
+        assert all("all-gather" in e or "all-to-allv" in e or "all-reduce" in e for e in errs), errs
+    finally:
+        for g in graphs:
+            g.free()
+        for c in ctxs:
+            c.close()
+
+
+def test_native_group_missing_rank_times_out(bfsx):
+    """A rank that never calls (it crashed without aborting, or took another path) is noticed by the deadline
+    (comm_timeout_ms): the waiting rank fails with "timed out" instead of hanging."""
+    world, scale, seed = 2, 12, 0x71AE
+    ctxs = [bfsx.Context(0, comm_timeout_ms="1500") for _ in range(world)]
+    graphs = []
+    try:
+        bfsx.local_group(ctxs)
+        graphs = [ctxs[r].dist_kronecker(scale, r, world, seed=seed) for r in range(world)]
+        src = int(O.kronecker(scale, 16, seed)[0][0])
+        err = []
+
+        def work():
+            try:
+                graphs[0].dist_bfs(src)
+            except bfsx.BfsxError as e:
+                err.append(str(e))
+
+        t = threading.Thread(target=work)
+        took = run_ranks_timed([t])
+        assert not t.is_alive() and err and "timed out" in err[0], err
+        assert 1.0 < took < 10.0, took
+    finally:
+        for g in graphs:
+            g.free()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_context_one_call(bfsx, world):
+    """bfsx_init_group (multi-GPU is internal, the caller sees one call): graphs built on a group
+    context are partitioned over its ranks, and bfsx_bfs / bfsx_result / bfsx_validate / bfsx_level_* return the
+    whole graph's result from one call.  On this one-GPU box the ranks share device 0 (in-process group); the
+    result equals the single-device one bit for bit, from an algs4 file (every rank tokenizes it on its GPU,
+    bfsx_dist_graph_load_algs4), a tuple list and the Kronecker generator."""
+    with bfsx.Context(group=world, **GROUP_DEFAULTS) as gc, bfsx.Context(0) as one:
+        assert gc.group_size == world and one.group_size == 1
+        for name in ("mediumG", "tinyCG"):
+            path = os.path.join(GOLDEN, name + ".txt")
+            with gc.load_algs4(path) as g, one.load_algs4(path) as g1:
+                assert g.nv == g1.nv and g.nnz == g1.nnz and g.m == g1.m
+                d, p, st = g.bfs(0)
+                d1, _, st1 = g1.bfs(0)
+                assert np.array_equal(d, d1)
+                ref = np.loadtxt(os.path.join(GOLDEN, name + ".dist"), dtype=np.int64)
+                assert np.array_equal(d.astype(np.int64), ref[:, 1] if ref.ndim == 2 else ref)
+                assert st["levels"] == st1["levels"] and st["m_comp"] == st1["m_comp"]
+                assert st["reached"] == st1["reached"]
+                assert g.validate()["errors"] == 0
+                nv, u, v = O.load_graphfileutil(path)
+                off, col = O.build_sets(nv, u, v)
+                assert O.validate(nv, off, col, 0, d, p, rows_sorted=False) == 0
+                assert len(g.level_times()) == st["levels"] and len(g.level_dirs()) == st["levels"]
+                ls = g.level_stats()
+                assert sum(x["frontier_out"] for x in ls) == st["reached"] - 1
+                d2, p2 = g.result()
+                assert np.array_equal(d2, d) and np.array_equal(p2, p)
+                goff, gcol = g.csr()
+                for x in range(0, nv, 7):
+                    assert set(gcol[goff[x]:goff[x + 1]].tolist()) == set(col[off[x]:off[x + 1]].tolist())
+        scale, seed = 14, 0x6A0B
+        u, v = O.kronecker(scale, 16, seed)
+        with gc.kronecker(scale, 16, seed) as g, gc.from_edges(1 << scale, u, v) as ge, \
+                one.kronecker(scale, 16, seed) as g1:
+            roots = g.sample_roots(4)
+            assert np.array_equal(roots, g1.sample_roots(4))
+            for r in roots.tolist():
+                d, p, st = g.bfs(r)
+                assert np.array_equal(d, g1.bfs(r)[0])
+                assert np.array_equal(ge.bfs(r)[0], d)
+                assert g.validate()["errors"] == 0 and st["t_bfs_ms"] > 0
+        with pytest.raises(bfsx.BfsxError):
+            with gc.kronecker(12, 16, 1) as g:
+                g.bfs(1 << 12)  # outside the graph: fails on every rank, and the group stays usable
+        with gc.kronecker(12, 16, 1) as g, one.kronecker(12, 16, 1) as g1:
+            assert np.array_equal(g.bfs(5)[0], g1.bfs(5)[0])

@@ -173,3 +173,45 @@ def test_bfs_spark_twin_bad_input(tmp_path):
     write_props(tmp_path, ["bad.txt"])
     r = subprocess.run([BIN], cwd=tmp_path, capture_output=True, text=True, timeout=60)
     assert r.returncode == 5 and "GraphFileUtil.convert failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_bfs_spark_twin_devices(tmp_path):
+    """devices=N (ServiceConfiguration.java:35-39 plus `devices`): one twin call runs the
+    1-D partitioned level loop on N ranks (bfsx_init_group; on a one-GPU box the ranks share the device as an
+    in-process group).  Every pass's problemFile_k holds the same fields as with devices=1: neighbour rows (in
+    the same HashSet order), distances and colours identical, paths of the same length -- each a shortest path
+    along graph edges (parents are tie-break dependent, BfsSpark.java:97)."""
+    names = ["tinyCG", "mediumG"]
+    passes = {"tinyCG": 3, "mediumG": 14}
+    out = {}
+    for dev in (1, 2, 3):
+        d = tmp_path / f"dev{dev}"
+        d.mkdir()
+        files = []
+        for n in names:
+            shutil.copy(os.path.join(GOLDEN, n + ".txt"), d / (n + ".txt"))
+            files.append(f"{n}.txt")
+        write_props(d, files, f"dumpLevels=true\nvalidate=true\ndevices={dev}\n")
+        r = subprocess.run([BIN], cwd=d, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.count("Validation: OK") == len(names)
+        if dev > 1:
+            assert f"{dev} ranks of a 1-D vertex partition" in r.stdout
+        out[dev] = d
+    for n in names:
+        nv, u, v = O.load_graphfileutil(str(tmp_path / "dev1" / f"{n}.txt"))
+        off, col = O.build_sets(nv, u, v)
+        dist = read_dist(n + ".dist")
+        for k in range(passes[n] + 1):
+            base = (out[1] / f"{n}.txt_{k}").read_text().split("\n")
+            check_state(read_state(out[1] / f"{n}.txt_{k}"), nv, off, col, dist, k)
+            for dev in (2, 3):
+                other = (out[dev] / f"{n}.txt_{k}").read_text().split("\n")
+                check_state(read_state(out[dev] / f"{n}.txt_{k}"), nv, off, col, dist, k)
+                assert len(other) == len(base)
+                for a, b in zip(base, other):
+                    ta, tb = a.split("|"), b.split("|")
+                    assert (ta[0], ta[1], ta[3], ta[4]) == (tb[0], tb[1], tb[3], tb[4])
+                    assert len(ta[2].split(",")) == len(tb[2].split(","))
+        assert not os.path.exists(out[2] / f"{n}.txt_{passes[n] + 1}")
