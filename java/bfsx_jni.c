@@ -66,6 +66,16 @@ JNIEXPORT jlong JNICALL Java_it_unitn_bd_bfs_Bfsx_init(JNIEnv *env, jclass cls, 
     return failed(env, bfsx_init(device, &ctx)) ? 0 : J(ctx);
 }
 
+JNIEXPORT jlong JNICALL Java_it_unitn_bd_bfs_Bfsx_initGroup(JNIEnv *env, jclass cls, jint nranks) {
+    bfsx_ctx *ctx = NULL;
+    return failed(env, bfsx_init_group(nranks, &ctx)) ? 0 : J(ctx);
+}
+
+JNIEXPORT jint JNICALL Java_it_unitn_bd_bfs_Bfsx_groupSize(JNIEnv *env, jclass cls, jlong ctx) {
+    const int n = bfsx_group_size(H(ctx));
+    return failed(env, n) ? 0 : n;
+}
+
 JNIEXPORT void JNICALL Java_it_unitn_bd_bfs_Bfsx_setOption(JNIEnv *env, jclass cls, jlong ctx, jstring key,
                                                           jstring value) {
     const char *k = (*env)->GetStringUTFChars(env, key, NULL);

@@ -9,6 +9,7 @@ import org.apache.logging.log4j.Logger;
 import java.io.BufferedReader;
 import java.io.FileInputStream;
 import java.io.IOException;
+import java.io.InputStream;
 import java.io.InputStreamReader;
 import java.nio.ByteBuffer;
 import java.nio.file.Files;
@@ -18,6 +19,7 @@ import java.util.ArrayList;
 import java.util.HashSet;
 import java.util.LinkedList;
 import java.util.List;
+import java.util.Properties;
 import java.util.Set;
 
 /**
@@ -30,8 +32,14 @@ import java.util.Set;
  * Added to the reference's source tree next to BfsSpark (it uses ServiceConfiguration, Vertex and
  * Color from there) with Bfsx.java, and run as
  *   java -Djava.library.path=<dir of libbfsx_jni.so and libbfsx.so> -cp <jar> it.unitn.bd.bfs.BfsGpu
- * System properties: bfsx.device (HIP ordinal, default 0), bfsx.direction (auto|topdown|bottomup),
- * bfsx.validate (true: Graph500 validation of every result on the device, logged).
+ * Options, each read from a system property (-Dbfsx.<key>) or else from the same service.properties key (the
+ * reference's keys are read by its ServiceConfiguration, ServiceConfiguration.java:35-39; these are added, with
+ * defaults that keep the reference's behaviour, SURVEY.md 5):
+ *   device (HIP ordinal, default 0);  devices (default 1; N > 1: N ranks of a 1-D vertex partition in this
+ *   process, Bfsx.initGroup -- one GPU each, or sharing the visible ones);  direction (auto|topdown|bottomup);
+ *   dumpLevels (true: every pass's problemFile_k, as the reference writes them, BfsSpark.java:115-116; default
+ *   false: problemFile_0 and the last pass only);  validate (true: Graph500 validation of every result on the
+ *   device, logged).
  *
  * Differences kept from the C++ twin (bfs-with-mapreduce_amd/host/bfsx_spark.cpp): the final file lists
  * vertices in id order (the reference's order is Spark's collectAsMap order, BfsSpark.java:110), and
@@ -44,17 +52,41 @@ public final class BfsGpu {
 
     private static final int SOURCE_VERTEX = 0; // GraphFileUtil.java:28
 
+    private static final Properties SERVICE = new Properties();
+
+    static {
+        // the same file ServiceConfiguration reads (ServiceConfiguration.java:18,30-33), for the added keys
+        try (InputStream in = new FileInputStream("service.properties")) {
+            SERVICE.load(in);
+        } catch (IOException e) {
+            logger.warn("service.properties not readable for the bfsx keys: " + e.getMessage());
+        }
+    }
+
     private BfsGpu() {
+    }
+
+    /** -Dbfsx.key, else the service.properties key, else the default. */
+    static String option(String key, String def) {
+        final String p = System.getProperty("bfsx." + key);
+        return p != null ? p : SERVICE.getProperty(key, def);
     }
 
     public static void main(String[] args) throws Exception {
         logger.info("Application name: " + ServiceConfiguration.getAppName());
         logger.info("Problem files path: " + ServiceConfiguration.getProblemFiles());
-        final int device = Integer.getInteger("bfsx.device", 0);
-        logger.info("Connecting to: HIP device " + device + " (libbfsx)");
-        final long ctx = Bfsx.init(device);
+        final int devices = Integer.parseInt(option("devices", "1"));
+        final long ctx;
+        if (devices > 1) {
+            logger.info("Connecting to: " + devices + " ranks of a 1-D vertex partition, one per HIP device (libbfsx)");
+            ctx = Bfsx.initGroup(devices);
+        } else {
+            final int device = Integer.parseInt(option("device", "0"));
+            logger.info("Connecting to: HIP device " + device + " (libbfsx)");
+            ctx = Bfsx.init(device);
+        }
         try {
-            Bfsx.setOption(ctx, "direction", System.getProperty("bfsx.direction", "auto"));
+            Bfsx.setOption(ctx, "direction", option("direction", "auto"));
             for (String problemFile : ServiceConfiguration.getProblemFiles()) {
                 logger.info("Problem file: " + problemFile);
                 run(ctx, problemFile);
@@ -73,10 +105,13 @@ public final class BfsGpu {
             write(problemFile + "_0", neighbours, null, null, 0); // the initial state (GraphFileUtil.java:68)
             final int passes = Bfsx.bfs(g, SOURCE_VERTEX, dist, parent); // BfsSpark.java:57-118
             final double[] cum = Bfsx.levelTimesMs(g);
-            for (int k = 1; k <= passes; k++)
+            final boolean dumpLevels = Boolean.parseBoolean(option("dumpLevels", "false"));
+            for (int k = 1; k <= passes; k++) {
                 logger.info("Elapsed time [" + k + "] ==> " + stopwatch(Math.round(cum[k - 1] * 1e6)));
-            write(problemFile + "_" + passes, neighbours, dist, parent, passes);
-            if (Boolean.getBoolean("bfsx.validate")) {
+                // the state after pass k, as the reference writes it every pass (BfsSpark.java:115-116)
+                if (dumpLevels || k == passes) write(problemFile + "_" + k, neighbours, dist, parent, k);
+            }
+            if (Boolean.parseBoolean(option("validate", "false"))) {
                 final long bad = Bfsx.validate(g);
                 logger.info(bad == 0 ? "Validation: OK (Graph500 rules, exact BFS distances)"
                                      : "Validation: " + bad + " violating vertices");
@@ -110,7 +145,11 @@ public final class BfsGpu {
         return sets;
     }
 
-    /** pass 0: the source GRAY, everything else WHITE; the last pass: reached BLACK, the rest WHITE. */
+    /**
+     * The state after pass `pass` (the map/reduce semantics of BfsSpark.java:66-108): pass 0 is the source GRAY,
+     * everything else WHITE; after pass k a vertex at distance d < k is BLACK, d == k GRAY (discovered by that
+     * pass), and d > k or unreachable WHITE with Integer.MAX_VALUE and the initial path [source].
+     */
     private static void write(String file, List<Set<Integer>> neighbours, ByteBuffer dist, ByteBuffer parent, int pass)
             throws IOException {
         final StringBuilder out = new StringBuilder();
@@ -123,15 +162,15 @@ public final class BfsGpu {
                                             : new Vertex(v, neighbours.get(v), start, Integer.MAX_VALUE, Color.WHITE);
             } else {
                 final int d = dist.getInt(4 * v);
-                if (d == Integer.MAX_VALUE) {
-                    vertex = new Vertex(v, neighbours.get(v), start, d, Color.WHITE);
+                if (d == Integer.MAX_VALUE || d > pass) {
+                    vertex = new Vertex(v, neighbours.get(v), start, Integer.MAX_VALUE, Color.WHITE);
                 } else {
                     final LinkedList<Integer> path = new LinkedList<>();
                     for (long x = v; ; x = parent.getLong(8 * (int) x)) {
                         path.addFirst((int) x);
                         if (x == SOURCE_VERTEX) break;
                     }
-                    vertex = new Vertex(v, neighbours.get(v), path, d, Color.BLACK);
+                    vertex = new Vertex(v, neighbours.get(v), path, d, d == pass ? Color.GRAY : Color.BLACK);
                 }
             }
             if (v > 0) out.append('\n'); // Joiner.on("\n") (BfsSpark.java:115)

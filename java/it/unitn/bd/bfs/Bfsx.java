@@ -32,6 +32,16 @@ public final class Bfsx {
     // ---- context: replaces new JavaSparkContext(...) + addJar (BfsSpark.java:50-51), spark.stop (:120) ----
     public static native long init(int device) throws IOException;
 
+    /**
+     * A group context of nranks ranks in this process (bfsx_init_group): graphs loaded on it are 1-D partitioned
+     * over the ranks (one per GPU; ranks share a GPU when fewer are visible) and every call below on such a graph
+     * runs all ranks and returns once -- the Spark workers of the reference's cluster (BfsSpark.java:44,50).
+     */
+    public static native long initGroup(int nranks) throws IOException;
+
+    /** Ranks of a context (1 for init). */
+    public static native int groupSize(long ctx);
+
     public static native void setOption(long ctx, String key, String value);
 
     public static native void finalizeContext(long ctx);

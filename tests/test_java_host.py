@@ -56,3 +56,17 @@ def test_java_sources_are_java7(name):
     text = _strip_comments(open(os.path.join(SRC, name)).read())
     hits = [(p, m.group(0)) for p in JAVA8 for m in re.finditer(p, text)]
     assert not hits, f"{name} uses APIs or syntax newer than Java 7: {hits}"
+
+
+def test_java_host_options_devices_and_dump_levels():
+    """BfsGpu honours `devices` (N ranks through Bfsx.initGroup, the group context of
+    bfsx_init_group) and `dumpLevels` (every pass's problemFile_k, BfsSpark.java:115-116), each from a system
+    property or the service.properties key, as the C++ twin does."""
+    text = _strip_comments(open(os.path.join(SRC, "BfsGpu.java")).read())
+    raw = open(os.path.join(SRC, "BfsGpu.java")).read()
+    assert re.search(r'option\("devices",\s*"1"\)', raw) and "Bfsx.initGroup(" in text
+    assert re.search(r'option\("dumpLevels",\s*"false"\)', raw)
+    # inside the per-pass loop: every pass written when dumpLevels, the last pass always
+    assert re.search(r"if\s*\(dumpLevels\s*\|\|\s*k\s*==\s*passes\)\s*write\(", text)
+    # GRAY for the vertices a pass discovered (d == pass), WHITE beyond it
+    assert "d == pass ? Color.GRAY : Color.BLACK" in raw and "d > pass" in raw
