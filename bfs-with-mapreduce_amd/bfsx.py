@@ -37,7 +37,7 @@ EXPORTS = [
     "bfsx_device_synchronize", "bfsx_validate", "bfsx_validate_result",
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
     "bfsx_last_bfs_ms", "bfsx_last_unpack_ms", "bfsx_persist_fallbacks", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group",
-    "bfsx_dist_bfs", "bfsx_init_group", "bfsx_group_size", "bfsx_dist_graph_load_algs4",
+    "bfsx_dist_bfs", "bfsx_init_group", "bfsx_group_size", "bfsx_dist_graph_load_algs4", "bfsx_last_resolve_ms",
 ]
 # test-only level primitives (include/bfsx_levels.h): exported for tests/dist_driver.py, not product ABI
 TEST_EXPORTS = [
@@ -112,6 +112,8 @@ def lib():
         L.bfsx_level_dirs.argtypes = [_VP, _VP, C.c_int]
         L.bfsx_last_bfs_ms.argtypes = [_VP, C.POINTER(C.c_double)]
         L.bfsx_last_unpack_ms.argtypes = [_VP, C.POINTER(C.c_double)]
+        if hasattr(L, "bfsx_last_resolve_ms") or not os.environ.get("BFSX_LIB"):  # an older build (A/B) may lack it
+            L.bfsx_last_resolve_ms.argtypes = [_VP, C.POINTER(C.c_double)]
         if hasattr(L, "bfsx_persist_fallbacks") or not os.environ.get("BFSX_LIB"):  # an older build (A/B) may lack it
             L.bfsx_persist_fallbacks.argtypes = [_VP, C.POINTER(C.c_int64)]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
@@ -336,6 +338,15 @@ class Graph:
         packed internal-id state -> original-id dist / parent arrays, outside t_bfs; -1 if none ran."""
         ms = C.c_double()
         _check(lib().bfsx_last_unpack_ms(self._h, C.byref(ms)))
+        return ms.value
+
+    def last_resolve_ms(self):
+        """Device time (ms) of the internal-id part of the most recent unpack (bfsx_last_resolve_ms): push log and
+        pull records folded into the per-vertex state; -1 if none ran (or an older build, BFSX_LIB)."""
+        if not hasattr(lib(), "bfsx_last_resolve_ms"):
+            return -1.0
+        ms = C.c_double()
+        _check(lib().bfsx_last_resolve_ms(self._h, C.byref(ms)))
         return ms.value
 
     def persist_fallbacks(self):

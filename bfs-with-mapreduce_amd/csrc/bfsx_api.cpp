@@ -1217,6 +1217,17 @@ int bfsx_last_unpack_ms(const bfsx_graph *g, double *ms) {
     return BFSX_OK;
 }
 
+int bfsx_last_resolve_ms(const bfsx_graph *g, double *ms) {
+    if (!g || !ms) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) {
+        *ms = -1.0;
+        for (const bfsx_graph *p : g->parts) *ms = std::max(*ms, bfs_last_resolve_ms(p));
+        return BFSX_OK;
+    }
+    *ms = bfs_last_resolve_ms(g);
+    return BFSX_OK;
+}
+
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap) {
     if (!g || (!dirs && cap > 0)) return fail(BFSX_E_ARG, "bad argument");
     if (is_group(g)) return bfsx_level_dirs(g->parts[0], dirs, cap); // all-reduced: the same on every rank

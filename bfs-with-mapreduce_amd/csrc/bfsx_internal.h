@@ -153,6 +153,9 @@ int64_t bfs_persist_fallbacks(const bfsx_graph *g); // BFS runs re-run without K
 int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out);
 // device time (ms) of the most recent copy's unpack kernel (state + level records -> original-id dist/parent); -1: none
 double bfs_last_unpack_ms(const bfsx_graph *g);
+// its first part: the push log scattered and the pull records folded into the per-vertex state (the result in
+// internal ids); -1 when the last copy took the scatter path (graphs without the relabel)
+double bfs_last_resolve_ms(const bfsx_graph *g);
 // multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
 int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue);

@@ -148,12 +148,19 @@ struct BfsWorkspace {
     // not be result data and whose result data must not be frontier ids -- and two pinned host chunks the D2H
     // copy streams through while host threads split them into the caller's arrays
     u64 *out64 = nullptr;
+    // the unpack's phase-1 words (k_resolve_all: parent_original << 32 | dist per INTERNAL id): the push log's
+    // buffer once the log is scattered (single device), else rtmp, allocated at the first copy
+    u64 *rtmp = nullptr;
+    // every id >= iso_lo names an empty row (1 + the largest non-empty row): on a relabelled graph the isolated
+    // tail of the degree order, half the ids of a scale-26 Kronecker graph
+    int64_t iso_lo = 0;
     int out_mode = 0;        // out64's fill: 0 none, 1 packed words, 2 int32 distances (isolated ids keep it)
     int64_t out_dirty = -1;  // an isolated vertex whose out64 entry the last unpack overwrote (it was the source)
     u64 *h_stage = nullptr;
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
-    hipEvent_t ev_unpack0 = nullptr, ev_unpack1 = nullptr;
+    hipEvent_t ev_unpack0 = nullptr, ev_unpack1 = nullptr, ev_unpack_mid = nullptr;
     double last_unpack_ms = -1.0;       // device time of the most recent unpack (state -> original-id arrays)
+    double last_resolve_ms = -1.0;      // its internal-id part: push log + records folded into st (-1: none)
     // mapped pinned word: 0, or 1 << 32 | id of the first out-of-range id a queue consumer met (id_ok)
     u64 *h_err = nullptr, *d_err = nullptr;
     LevelSlot *ring = nullptr;          // device, 3 slots
@@ -2266,27 +2273,56 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, con
     }
 }
 
-// The same in ORIGINAL id order (a relabelled graph, round 4): thread o reads perm[o] and writes out[o], so the
-// writes are whole lines.  The reads stay near-sequential: the relabel sorts by degree with ties in original
-// order, so the vertices of one degree class keep their original order in the internal ids -- consecutive
-// original ids read K advancing streams (one per degree class present), whose lines L2 holds.  Every entry is
-// written (isolated ones as unreached, except the source), so no prefill is needed.  The scatter form above
-// writes one 8-B word per 64-B line (consecutive internal ids of a class are original ids several apart).
-__global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
-                                                       RecSet rs, const uint32_t *__restrict__ perm,
-                                                       const uint32_t *__restrict__ inv, int64_t n,
-                                                       const u64 *__restrict__ dead, int64_t src,
-                                                       u64 *__restrict__ out, int32_t *__restrict__ dist_only) {
+// The result in ORIGINAL id order (a relabelled graph), in two passes (round 5; round 4 ran one gather of
+// 0.685 ms per scale-26 result whose every entry chained perm -> dead word -> one record word per pull level ->
+// st or par -> inv, each a dependent gather):
+//   phase 1, k_resolve_all, INTERNAL id order: one wave per 64-vertex bitmap word, lane = bit.  The word's record
+//     words are broadcast loads issued together; par, st and tmp are coalesced.  A record vertex's state
+//     (par[i], the record's distance) is stored into st, so st ends resolved (parents in internal ids: the
+//     Graph500 kernel-2 result on the device, which the validator and m_comp read), and with tmp every live i
+//     gets tmp[i] = parent_original << 32 | dist, the parent mapped through inv here, where the parents of
+//     consecutive vertices are the same few hubs (inv lines stay cached).  Only the words below iso_lo (the
+//     isolated tail) and the source's word are visited.
+//   phase 2, k_unpack_gather: thread o reads perm[o] and copies tmp[perm[o]] into out[o] -- whole-line writes,
+//     near-sequential reads (the relabel keeps original order inside a degree class) -- or writes the unreached
+//     word without a load for an id of the isolated tail.
+__global__ __launch_bounds__(kBS) void k_resolve_all(RecSet rs, int64_t nwords_live, int64_t src_word,
+                                                     const uint32_t *__restrict__ par, u64 *__restrict__ stt,
+                                                     const uint32_t *__restrict__ inv, u64 *__restrict__ tmp,
+                                                     int64_t n) {
+    const unsigned lane = lane_id();
+    const int64_t nwaves = ((int64_t)gridDim.x * kBS) >> 6;
+    const int64_t nit = nwords_live + (src_word >= nwords_live ? 1 : 0);
+    for (int64_t it = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; it < nit; it += nwaves) {
+        const int64_t w = it < nwords_live ? it : src_word;
+        int hit = -1;
+#pragma unroll 4
+        for (int r = 0; r < rs.n; r++) // records are disjoint: the loads are independent
+            if ((rs.bm[r][w] >> lane) & 1ull) hit = r;
+        const int64_t v = w * 64 + lane;
+        if (v >= n) continue;
+        u64 s;
+        if (hit >= 0) {
+            s = pack_state(par[v], rs.nd[hit]);
+            stt[v] = s;
+        } else {
+            s = stt[v];
+        }
+        if (tmp) {
+            const uint32_t p = (uint32_t)(s >> 32);
+            tmp[v] = ((u64)(p == 0xFFFFFFFFu ? p : inv[p]) << 32) | (uint32_t)s;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ tmp, const uint32_t *__restrict__ perm,
+                                                       int64_t n, int64_t iso_lo, int64_t src, u64 *__restrict__ out,
+                                                       int32_t *__restrict__ dist_only) {
     for (int64_t o = (int64_t)blockIdx.x * kBS + threadIdx.x; o < n; o += (int64_t)gridDim.x * kBS) {
         const int64_t i = (int64_t)perm[o];
-        u64 s = kUnreached;
-        if (!((dead[i >> 6] >> (i & 63)) & 1ull) || i == src) s = rec_state(stt, par, rs, i);
-        if (dist_only) {
-            dist_only[o] = (int32_t)(uint32_t)s;
-        } else {
-            const uint32_t p = (uint32_t)(s >> 32);
-            out[o] = ((u64)(p == 0xFFFFFFFFu ? p : inv[p]) << 32) | (uint32_t)s;
-        }
+        const u64 s = (i >= iso_lo && i != src) ? kUnreached : tmp[i];
+        if (dist_only) dist_only[o] = (int32_t)(uint32_t)s;
+        else out[o] = s;
     }
 }
 
@@ -2638,7 +2674,7 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&ws->d_err, ws->h_err, 0));
     *ws->h_err = 0;
     BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(u64)));
-    BFSX_HIP_TRY(hipMalloc(&ws->d_red, 2 * sizeof(u64)));
+    BFSX_HIP_TRY(hipMalloc(&ws->d_red, 3 * sizeof(u64)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_end));
     const unsigned gfill = clamp_grid(((int64_t)nv + kBS - 1) / kBS, 8192);
@@ -2661,17 +2697,20 @@ int ws_alloc(bfsx_graph *g) {
     hipLaunchKernelGGL(k_dead_mask, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 4096)), dim3(kBS), 0, st,
                        g->d_row_off, g->d_col, g->nv, ws->nwords, (uint32_t)g->v_lo, ws->dead);
     BFSX_LAUNCHED(st);
-    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 2 * sizeof(u64), st));
+    BFSX_HIP_TRY(hipMemsetAsync(ws->d_red, 0, 3 * sizeof(u64), st));
     hipLaunchKernelGGL(k_popc, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, 2048)), dim3(kBS), 0, st, ws->dead,
                        ws->nwords, ws->d_red);
     BFSX_LAUNCHED(st);
     hipLaunchKernelGGL(k_rows_above, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, (int64_t)1, ws->d_red + 1);
     BFSX_LAUNCHED(st);
-    u64 nd[2] = {0, 0};
+    hipLaunchKernelGGL(k_rows_above, dim3(gfill), dim3(kBS), 0, st, g->d_row_off, g->nv, (int64_t)0, ws->d_red + 2);
+    BFSX_LAUNCHED(st);
+    u64 nd[3] = {0, 0, 0};
     BFSX_HIP_TRY(hipMemcpyAsync(nd, ws->d_red, sizeof(nd), hipMemcpyDeviceToHost, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st));
     ws->n_dead = (int64_t)nd[0] - (ws->nwords * 64 - g->nv); // minus padding bits
     ws->leaf_lo = (int64_t)nd[1];
+    ws->iso_lo = (int64_t)nd[2];
     return BFSX_OK;
 }
 
@@ -3141,7 +3180,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
-                    (void *)ws->d_dist_ctr, (void *)ws->out64})
+                    (void *)ws->d_dist_ctr, (void *)ws->out64, (void *)ws->rtmp})
         if (p) (void)hipFree(p);
     for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
     for (void *p : ws->prec) (void)hipFree(p);
@@ -3151,6 +3190,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     if (ws->h_err) (void)hipHostFree(ws->h_err);
     if (ws->ev_unpack0) (void)hipEventDestroy(ws->ev_unpack0);
     if (ws->ev_unpack1) (void)hipEventDestroy(ws->ev_unpack1);
+    if (ws->ev_unpack_mid) (void)hipEventDestroy(ws->ev_unpack_mid);
     for (auto e : ws->ev_stage)
         if (e) (void)hipEventDestroy(e);
     if (ws->h_stage) (void)hipHostFree(ws->h_stage);
@@ -3697,6 +3737,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         BFSX_HIP_TRY(hipMalloc(&ws->out64, std::max<size_t>(nv, 1) * sizeof(u64)));
         BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack0));
         BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack1));
+        BFSX_HIP_TRY(hipEventCreate(&ws->ev_unpack_mid));
     }
     RecSet rs{};
     rs.n = ws->resolved ? 0 : ws->n_prec;
@@ -3734,8 +3775,20 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     }
     if (int e = apply_logs(g, ws, ws->ev_unpack0)) return e; // the push log is part of the unpack's time
     if (gather) {
-        hipLaunchKernelGGL(k_unpack_gather, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_perm, g->d_inv,
-                           (int64_t)nv, ws->dead, src, ws->out64, d_dist_only);
+        u64 *tmp = ws->plog; // free once the log is scattered (apply_logs above)
+        if (!tmp) {
+            if (!ws->rtmp) BFSX_HIP_TRY(hipMalloc(&ws->rtmp, std::max<size_t>(nv, 1) * sizeof(u64)));
+            tmp = ws->rtmp;
+        }
+        const int64_t nw_live = std::min<int64_t>((ws->iso_lo + 63) / 64, ws->nwords);
+        const int64_t src_word = src >= 0 ? src / 64 : 0;
+        hipLaunchKernelGGL(k_resolve_all, dim3(clamp_grid((nw_live + 1 + kWaves - 1) / kWaves, 8192)), dim3(kBS), 0, st,
+                           rs, nw_live, src_word, ws->par, ws->st, g->d_inv, tmp, (int64_t)nv);
+        BFSX_LAUNCHED(st);
+        ws->resolved = true; // st now holds every record vertex's state too (bfs_resolve has nothing left to do)
+        BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack_mid, st));
+        hipLaunchKernelGGL(k_unpack_gather, grid, dim3(kBS), 0, st, tmp, g->d_perm, (int64_t)nv, ws->iso_lo, src,
+                           ws->out64, d_dist_only);
         ws->out_mode = 0; // every entry written: a later scatter-mode unpack must prefill again
     } else if (g->d_inv)
         hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo, (int64_t)nv,
@@ -3800,10 +3853,16 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
     float ms = 0.f;
     BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_unpack0, ws->ev_unpack1));
     ws->last_unpack_ms = ms;
+    ws->last_resolve_ms = -1.0;
+    if (gather) {
+        BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_unpack0, ws->ev_unpack_mid));
+        ws->last_resolve_ms = ms;
+    }
     return BFSX_OK;
 }
 
 double bfs_last_unpack_ms(const bfsx_graph *g) { return g->ws ? g->ws->last_unpack_ms : -1.0; }
+double bfs_last_resolve_ms(const bfsx_graph *g) { return g->ws ? g->ws->last_resolve_ms : -1.0; }
 
 // ==== multi-GPU level primitives (1-D partition) ====================================================
 // The product runs the partitioned level loop natively (dist_bfs_run below, exchanges through

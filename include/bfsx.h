@@ -228,6 +228,11 @@ int bfsx_persist_fallbacks(const bfsx_graph *g, int64_t *count);
  * ORIGINAL id (parent, dist) that the outputs are split from.  It runs after t_bfs (outside the timed region),
  * before the D2H copy; -1 if no copy ran yet. */
 int bfsx_last_unpack_ms(const bfsx_graph *g, double *ms);
+/* Device time (ms) of the first part of that unpack: the push levels' log scattered and the pull levels' records
+ * folded into the per-vertex state, so that a distance and a parent exist for every vertex in the graph's
+ * internal (degree-ordered) ids -- Graph500 kernel 2's output, before the translation to the caller's ids; -1 if
+ * the last copy did not run it (graphs built with "relabel" off unpack in one scatter pass). */
+int bfsx_last_resolve_ms(const bfsx_graph *g, double *ms);
 /* Per-level direction of the most recent bfsx_bfs: BFSX_DIR_TOPDOWN (1), BFSX_DIR_BOTTOMUP (2), BFSX_DIR_HYBRID (3)
  * or BFSX_DIR_BOTTOMUP_SPARSE (4). */
 int bfsx_level_dirs(bfsx_graph *g, int32_t *dirs, int cap);

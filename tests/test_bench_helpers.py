@@ -35,7 +35,9 @@ def test_top_down_level_bytes(bench):
 
 def test_hybrid_level_bytes(bench):
     ls = {"direction": 3, "unvisited_in": 1000, "scanned": 300, "frontier_out": 20}
-    assert bench.level_bytes(ls, 64) == 16 * 64 + 4 * 1000 + 4 * 300 + 8 * 20
+    # both halves of a hybrid level store the 4-B parent: found_bytes per discovery, like a pull level
+    assert bench.level_bytes(ls, 64) == 16 * 64 + 4 * 1000 + 4 * 300 + 4 * 20
+    assert bench.level_bytes(ls, 64, found_bytes=8) == 16 * 64 + 4 * 1000 + 4 * 300 + 8 * 20
 
 
 def test_level_account_whole_bfs(bench):
