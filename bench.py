@@ -171,23 +171,36 @@ def common_fields(args, world, value, wall, nv, m, nnz, nroots, parallelism):
     }
 
 
+# The BFS kernel sources (one translation unit per kernel family + their shared core): a PMC summary is reported
+# only for the source it was measured on, hashed as the concatenation in this order (tools/pmc_summary.py and the
+# profiling scripts: cat <these files> | sha256sum)
+BFS_SRCS = ("bfs_core.h", "kernels_push.hip", "kernels_pull.hip", "kernels_persist.hip", "kernels_level.hip",
+            "kernels_dist.hip")
+
+
+def bfs_src_sha(pkg=None):
+    import hashlib
+    h = hashlib.sha256()
+    for f in BFS_SRCS:
+        h.update(open(os.path.join(pkg or PKG, "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def measured_traffic(kernel="k_bu", nwords=None):
     """Per-launch HBM bytes of `kernel` from the newest committed PMC summary (profiles/<tag>_hbm.json,
     written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes),
-    used only while kernels_bfs.hip still hashes to the source it was measured on, and only for the graph
-    size it was measured on (nwords: bitmap words of the bench's graph; a scale-26 profile says nothing
-    about a scale-30 launch)."""
+    used only while the BFS kernel sources (BFS_SRCS) still hash to the source they were measured on, and only
+    for the graph size it was measured on (nwords: bitmap words of the bench's graph; a scale-26 profile says
+    nothing about a scale-30 launch)."""
     import glob
-    import hashlib
-    src = os.path.join(PKG, "csrc", "kernels_bfs.hip")
-    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    sha = bfs_src_sha()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm.json")), reverse=True):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
         names = [n for n in rec.get("kernels", {}) if n == kernel or n.startswith(kernel + "<")]
-        if rec.get("kernels_bfs_sha") == sha and names and (nwords is None or rec.get("nwords") == nwords):
+        if rec.get("bfs_src_sha") == sha and names and (nwords is None or rec.get("nwords") == nwords):
             # the instantiation with the most launches (the hybrid levels' hub sweep is a second one)
             k = max((rec["kernels"][n] for n in names), key=lambda x: x.get("launches", 0))
             # per-access-class correction when the summary has it (round 3: profiles/r03k_fetch_calibration.json),
@@ -321,6 +334,10 @@ def cpu_baselines(args, g, roots, mcomp, nv):
         "affinity_cpus": affinity,
         "threads_from": ("--cpu-threads" if args.cpu_threads else
                          "OMP_NUM_THREADS (the job's CPU share on the GPU box)" if env_threads else "sched_getaffinity"),
+        "threads_note": ("the GPU box gives one GPU's job a share of 16 host threads and sets OMP_NUM_THREADS=16, which "
+                         "jobs must leave as it is; the affinity mask (affinity_cpus) and nproc show the whole host, whose "
+                         "other CPUs serve the other GPUs' jobs.  --cpu-threads N runs the row on N threads instead"
+                         if env_threads and not args.cpu_threads else None),
         "kind": "port",
         "sample": f"{len(samples)} root(s) of the same scale-{args.scale} graph, oracle orc_mapreduce_bfs "
                   f"(BfsSpark map/reduce restated, OpenMP), {spent:.1f} s; distances asserted equal to the GPU's",

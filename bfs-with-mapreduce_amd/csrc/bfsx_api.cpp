@@ -3,7 +3,7 @@
 //
 // Host side of the drop-in boundary: error plumbing, the algs4 edge-list parser with
 // GraphFileUtil.convert semantics (GraphFileUtil.java:45-66), graph handles, root sampling and the
-// synchronous bfsx_bfs wrapper around the device level loop (kernels_bfs.hip).
+// synchronous bfsx_bfs wrapper around the device level loops (kernels_level.hip, kernels_dist.hip).
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -392,6 +392,16 @@ int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value) {
 
 static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
     const std::string k(key), v(value);
+#ifndef BFSX_DIAG
+    // test hooks and diagnostics exist in the diagnostic library only (libbfsx_diag.so, built with BFSX_DIAG);
+    // "off" is accepted (a no-op) so that a caller resetting them needs no special case
+    for (const char *d : {"poison_queues", "test_overread", "bu_force_spill", "persist_abort_at", "check_retired", "fail_at"})
+        if (k == d) {
+            if (v == "off") return BFSX_OK;
+            return fail(BFSX_E_ARG, k + " is a test hook of the diagnostic library (libbfsx_diag.so, built with "
+                                        "BFSX_DIAG); the product library does not compile it");
+        }
+#endif
     auto as_int = [&](int &dst) -> int {
         char *end = nullptr;
         long x = strtol(value, &end, 10);

@@ -145,7 +145,7 @@ int build_csr_kronecker(hipStream_t stream, int scale, int edgefactor, uint64_t 
 // each row keeps its degree-descending order).  row_off[nv+1] / col[nnz] host, either may be null.
 int export_csr_original(hipStream_t stream, int64_t nv, int64_t nnz, const int64_t *d_row_off, const uint32_t *d_col,
                         const uint32_t *d_perm, const uint32_t *d_inv, int64_t *row_off, uint32_t *col);
-// ---- kernels_bfs.hip ---------------------------------------------------------------------
+// ---- the BFS kernel families (bfs_core.h; kernels_{push,pull,persist,level,dist}.hip) -------------
 struct BfsWorkspace;
 int bfs_run(bfsx_graph *g, int64_t source, bfsx_stats *stats);
 int bfs_mcomp(bfsx_graph *g, int64_t *m_comp, int64_t *reached);
@@ -156,7 +156,7 @@ double bfs_last_unpack_ms(const bfsx_graph *g);
 // its first part: the push log scattered and the pull records folded into the per-vertex state (the result in
 // internal ids); -1 when the last copy took the scatter path (graphs without the relabel)
 double bfs_last_resolve_ms(const bfsx_graph *g);
-// multi-GPU level primitives (kernels_bfs.hip), driven by bfsx_dist_* in bfsx_api.cpp
+// multi-GPU level primitives (kernels_dist.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
 int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue);
 int dist_td_expand(bfsx_graph *g, unsigned long long *d_send, int64_t send_cap, int64_t *send_counts);

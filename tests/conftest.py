@@ -23,6 +23,8 @@ def load_bfsx():
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libbfsx.so on cuda:0)")
+    config.addinivalue_line("markers", "diag: the test's `ctx` is a context of the diagnostic library "
+                                       "(libbfsx_diag.so: test hooks, the encoded hub domain)")
 
 
 @pytest.fixture(scope="session")
@@ -30,15 +32,33 @@ def bfsx():
     return load_bfsx()
 
 
-@pytest.fixture(scope="session")
-def ctx(bfsx):
-    c = bfsx.Context(0)
-    # The test graphs are small: under the default push -> pull floor (pull_min_edges, 2^16 frontier edges)
-    # most of them would never pull, and the pull kernels would go untested.  The suite keeps round 2's
-    # floor (n/512 alone); tests/test_gpu_parity.py::test_pull_floor_default covers the default.
-    c.set_option("pull_min_edges", "0")
-    yield c
-    c.close()
+_CTX = {}
+
+
+def _session_ctx(bfsx, diag):
+    if diag not in _CTX:
+        c = bfsx.Context(0, diag=diag)
+        # The test graphs are small: under the default push -> pull floor (pull_min_edges, 2^16 frontier edges)
+        # most of them would never pull, and the pull kernels would go untested.  The suite keeps round 2's
+        # floor (n/512 alone); tests/test_gpu_parity.py::test_pull_floor_default covers the default.
+        c.set_option("pull_min_edges", "0")
+        _CTX[diag] = c
+    return _CTX[diag]
+
+
+@pytest.fixture(scope="session", autouse=False)
+def _ctx_cleanup():
+    yield
+    for c in _CTX.values():
+        c.close()
+    _CTX.clear()
+
+
+@pytest.fixture
+def ctx(request, bfsx, _ctx_cleanup):
+    """One device context per library for the whole session: the product library's, or for a test marked
+    `diag` (test hooks, the encoded hub domain) the diagnostic library's."""
+    return _session_ctx(bfsx, request.node.get_closest_marker("diag") is not None)
 
 
 @pytest.fixture(scope="session")

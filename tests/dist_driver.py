@@ -1,7 +1,7 @@
 """Test infrastructure: a Python restatement of the partitioned level loop over libbfsx's level
 primitives (bfsx_dist_begin / td_expand / td_claim / frontier_slice / bu_step / level_end / finish),
 with the exchange over torch.distributed.  The product loop is the native bfsx_dist_bfs
-(csrc/kernels_bfs.hip dist_bfs_run over csrc/bfsx_comm.cpp); this driver is the protocol reference the
+(csrc/kernels_dist.hip dist_bfs_run over csrc/bfsx_comm.cpp); this driver is the protocol reference the
 CPU (gloo, numpy engine) and GPU tests compare it with, and shows how a caller with its own exchange
 drives the primitives.  1-D vertex partition, one process per GPU.
 
@@ -182,7 +182,7 @@ class DistBFS:
         levels = 0
         while True:
             if self.direction == "auto" and levels > 0:
-                # Beamer's rule plus the exchange cost, as the native loop (kernels_bfs.hip
+                # Beamer's rule plus the exchange cost, as the native loop (kernels_dist.hip
                 # dist_bfs_run): pull once a top-down level's pairs would outweigh the bitmap all-gather
                 world = self.c.world
                 pairs_heavy = world > 1 and mf * 64 * (world - 1) > self.nv_global * world

@@ -34,10 +34,27 @@ def test_library_exports_every_declared_symbol():
     assert L.bfsx_abi_version() == 1
 
 
-def test_exports_are_plain_c_symbols():
-    out = os.popen(f"nm -D --defined-only {os.path.join(ROOT, 'bfs-with-mapreduce_amd', 'libbfsx.so')}").read()
+@pytest.mark.parametrize("so", ["libbfsx.so", "libbfsx_diag.so"])
+def test_exports_are_plain_c_symbols(so):
+    out = os.popen(f"nm -D --defined-only {os.path.join(ROOT, 'bfs-with-mapreduce_amd', so)}").read()
     for n in declared_functions():
         assert re.search(rf"\bT {n}$", out, flags=re.M), n
+
+
+def test_diagnostics_only_in_the_diagnostic_library():
+    """VERDICT r4 hygiene: the spilling pull kernel (k_bu_spill), the encoded hub-domain kernels of relabel=off
+    graphs and the queue-poisoning hook exist only in libbfsx_diag.so (built with -DBFSX_DIAG); the product
+    library refuses the hook options (tests/test_gpu_regress.py::test_product_library_refuses_test_hooks)."""
+    pkg = os.path.join(ROOT, "bfs-with-mapreduce_amd")
+
+    def kernels(so):
+        return os.popen(f"/opt/rocm/lib/llvm/bin/llvm-readelf -Ws --wide {os.path.join(pkg, so)} 2>/dev/null").read() \
+            + os.popen(f"nm -C {os.path.join(pkg, so)} 2>/dev/null").read()
+    prod, diag = kernels("libbfsx.so"), kernels("libbfsx_diag.so")
+    for sym in ("k_bu_spill", "k_hub_gather", "k_hub_encode"):
+        assert sym in diag, sym
+        assert sym not in prod, sym
+    assert "k_bu<" in prod and "k_td_persist<" in prod
 
 
 @pytest.mark.parametrize("name", ["tinyCG.txt", "mediumG.txt", "tinyG.txt"])

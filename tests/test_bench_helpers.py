@@ -83,14 +83,17 @@ def test_hmean(bench):
 
 
 def test_measured_traffic_requires_matching_source(bench, tmp_path, monkeypatch):
-    """A PMC summary counts only while kernels_bfs.hip still hashes to the source it was measured on;
-    of several k_bu instantiations the one with the most launches is reported."""
+    """A PMC summary counts only while the BFS kernel sources (bench.BFS_SRCS) still hash to the source it was
+    measured on; of several k_bu instantiations the one with the most launches is reported."""
     import hashlib
-    src = os.path.join(ROOT, "bfs-with-mapreduce_amd", "csrc", "kernels_bfs.hip")
-    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for f in bench.BFS_SRCS:
+        h.update(open(os.path.join(ROOT, "bfs-with-mapreduce_amd", "csrc", f), "rb").read())
+    sha = h.hexdigest()[:16]
+    assert sha == bench.bfs_src_sha()
     prof = tmp_path / "profiles"
     prof.mkdir()
-    rec = {"kernels_bfs_sha": sha, "fetch_correction": 2.0,
+    rec = {"bfs_src_sha": sha, "fetch_correction": 2.0,
            "kernels": {"k_bu<a, true>": {"launches": 2, "traffic_B": 9e9, "traffic_raw_B": 5e9, "avg_ms_trace": 1.0},
                        "k_bu<a, false>": {"launches": 90, "traffic_B": 1.2e9, "traffic_raw_B": 7e8,
                                           "avg_ms_trace": 0.25}}}
@@ -104,7 +107,7 @@ def test_measured_traffic_requires_matching_source(bench, tmp_path, monkeypatch)
     (prof / "zz_hbm.json").write_text(json.dumps(rec))
     assert bench.measured_traffic(nwords=1 << 20)["traffic"] == 1200.0
     assert bench.measured_traffic(nwords=1 << 24)["traffic"] is None
-    rec["kernels_bfs_sha"] = "0" * 16
+    rec["bfs_src_sha"] = "0" * 16
     (prof / "zz_hbm.json").write_text(json.dumps(rec))
     assert bench.measured_traffic()["traffic"] is None
 

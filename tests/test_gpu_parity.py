@@ -298,6 +298,7 @@ def test_push_log_matches_state_stores(ctx, persist):
         ctx.set_option("persist", "on")
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("abort_at", [0, 3])
 def test_persistent_abort_falls_back(ctx, abort_at):
     """A K3p launch whose grid barrier gives up (here: the "persist_abort_at" hook, the same exit path a
@@ -324,6 +325,7 @@ def test_persistent_abort_falls_back(ctx, abort_at):
         ctx.set_option("persist_abort_at", "off")
 
 
+@pytest.mark.diag
 def test_persistent_abort_time_covers_both_attempts(ctx):
     """t_bfs of a BFS whose K3p launch aborted covers the aborted attempt AND the re-run (round-3 verdict: the
     re-run re-recorded the start event, so the aborted attempt's time fell out of t_bfs).  A 1,100-vertex path:
@@ -441,6 +443,7 @@ def test_repeated_bfs_reuses_state(ctx):
         assert np.array_equal(d2, d0)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("bits", ["off", "1", "6", "12", "30"])
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
@@ -513,6 +516,7 @@ def test_chunked_csr_build(ctx, chunk, relabel):
         ctx.set_option("relabel", "on")
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("unroll", ["2", "4", "4-nopipe", "4-noprefix"])
 def test_bottomup_unroll_variants(ctx, unroll, relabel):
@@ -545,6 +549,7 @@ def test_bottomup_unroll_variants(ctx, unroll, relabel):
             ctx.set_option(k, val)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("bits", ["2", "6", "30"])
 def test_hybrid_levels(ctx, bits, relabel):
@@ -687,6 +692,7 @@ def test_leaf_skip(ctx):
         ctx.set_option("leaf_skip", "on")
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("floor", ["0", "65536"])
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
 @pytest.mark.parametrize("sparse", ["1", "64", "off"])
@@ -735,6 +741,7 @@ def _star_of_hubs(nhub, fan, tail):
     return nv, np.concatenate(u).astype(np.uint32), np.concatenate(v).astype(np.uint32)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("floor", ["0", "65536"])
 @pytest.mark.parametrize("dmax", ["2048", "64", "8"])
 def test_persistent_heavy_rows(ctx, dmax, floor):

@@ -17,7 +17,7 @@ import oracle_py as O
 from conftest import load_bfsx
 from test_gpu_parity import check_against_oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.diag]  # test hooks: the diagnostic library
 INF = 2147483647
 
 
@@ -165,3 +165,18 @@ def test_spilling_pull_kernel_partitioned_group(bfsx, world):
     out = run_group(bfsx, world, lambda c, r, w: c.dist_kronecker(scale, r, w, 16, 91), sources, "bottomup",
                     options={"bu_force_spill": "on", "poison_queues": "on"})
     check(nv, ou, ov, sources, out)
+
+
+def test_product_library_refuses_test_hooks(bfsx):
+    """The product library compiles no test hook: setting one fails loudly (only "off" is accepted, a no-op);
+    the diagnostic library takes it."""
+    with bfsx.Context(0) as c:
+        assert not c.diag
+        for k, val in (("poison_queues", "on"), ("test_overread", "0"), ("bu_force_spill", "on"),
+                       ("persist_abort_at", "3"), ("check_retired", "on"), ("fail_at", "0:1")):
+            with pytest.raises(bfsx.BfsxError, match="diagnostic library"):
+                c.set_option(k, val)
+            c.set_option(k, "off")
+    with bfsx.Context(0, poison_queues="on") as d:
+        assert d.diag
+        d.set_option("test_overread", "off")

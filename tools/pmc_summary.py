@@ -5,8 +5,8 @@
 Reads gpurun_out/<tag>/{trace,pmc_fetch,pmc_write}/ and writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   profiles/<tag>_hbm.json           per-launch HBM bytes of the dominant BFS kernels from the PMC passes,
-                                    with the source hash of kernels_bfs.hip they were measured on (bench.py
-                                    reports `roofline.traffic` only while that hash still matches)
+                                    with the hash of the BFS kernel sources they were measured on (bench.py
+                                    BFS_SRCS; bench.py reports `roofline.traffic` only while that hash matches)
   profiles/<tag>_bench.json         the default bench line of the same session (copied)
 
 Units and corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950
@@ -23,11 +23,15 @@ import statistics as S
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KSRC = os.path.join(ROOT, "bfs-with-mapreduce_amd", "csrc", "kernels_bfs.hip")
+BFS_SRCS = ("bfs_core.h", "kernels_push.hip", "kernels_pull.hip", "kernels_persist.hip", "kernels_level.hip",
+            "kernels_dist.hip")  # as bench.py BFS_SRCS
 
 
 def src_hash():
-    return hashlib.sha256(open(KSRC, "rb").read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for f in BFS_SRCS:
+        h.update(open(os.path.join(ROOT, "bfs-with-mapreduce_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def short(name):
@@ -75,7 +79,7 @@ def main():
         sha = open(os.path.join(d, "src_sha")).read().split()[0][:16]
     except OSError:
         sha = src_hash()
-    res = {"tag": tag, "kernels_bfs_sha": sha, "nwords": nwords, "fetch_correction": corr,
+    res = {"tag": tag, "bfs_src_sha": sha, "nwords": nwords, "fetch_correction": corr,
            "fetch_correction_basis": "k_finalize reads exactly 8*nwords B (8 B/lane coalesced)"
            if "k_finalize" in fetch else "guide default (x2 for wide streaming reads)",
            "kernels": {}}

@@ -12,7 +12,7 @@ STEPS=${2:-2}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT/calib"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-sha256sum bfs-with-mapreduce_amd/csrc/kernels_bfs.hip > "$OUT/src_sha"
+(cd bfs-with-mapreduce_amd/csrc && cat bfs_core.h kernels_push.hip kernels_pull.hip kernels_persist.hip kernels_level.hip kernels_dist.hip | sha256sum) > "$OUT/src_sha"
 B="python3 bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-p1"
 timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 timeout -k 10 120 tools/fetch_calib > "$OUT/calib/calib.json" 2> "$OUT/calib/calib.err"
