@@ -119,6 +119,14 @@ struct BfsWorkspace {
     // them distance prec_lvl[k] + 1.  st[v] of such a vertex is stale until bfs_resolve (or the fused unpack)
     // reads the records -- outside the timed region, like the unpack to original ids.
     uint32_t *par = nullptr;
+    // how each pull discovery's parent is named (kCodeTop1 .. kCodeExplicit); single device only (null on a
+    // partition, whose pull levels store every parent explicitly)
+    uint8_t *pcode = nullptr;
+    // the original ids of top1 / rest (relabelled graphs; the unpack's parents of code 0-3 without an inv gather),
+    // built at the first unpack when the device has room for them (else the unpack maps through inv)
+    uint32_t *otop1 = nullptr;
+    uint4 *orest = nullptr;
+    bool orig_nbrs_tried = false;
     std::vector<u64 *> prec;            // record pool (grown on demand, kept across BFS runs)
     std::vector<int32_t> prec_nd;       // distance of record k's vertices (its level + 1), last BFS
     int n_prec = 0;                     // records of the last BFS
@@ -167,7 +175,7 @@ struct BfsWorkspace {
     // not be result data and whose result data must not be frontier ids -- and two pinned host chunks the D2H
     // copy streams through while host threads split them into the caller's arrays
     u64 *out64 = nullptr;
-    // the unpack's phase-1 words (k_resolve_all: parent_original << 32 | dist per INTERNAL id): the push log's
+    // the unpack's phase-1 words (k_unpack_live: parent_original << 32 | dist per INTERNAL id): the push log's
     // buffer once the log is scattered (single device), else rtmp, allocated at the first copy
     u64 *rtmp = nullptr;
     // every id >= iso_lo names an empty row (1 + the largest non-empty row): on a relabelled graph the isolated
@@ -722,12 +730,36 @@ struct RecSet {
     int n;
 };
 
-// state of internal vertex i: st[i], unless a record holds i (its parent is then par[i]).  Lanes of consecutive
-// i share their record words (one broadcast load per wave and record).
-__device__ __forceinline__ u64 rec_state(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
-                                         const RecSet &rs, int64_t i) {
+// How a pull level found a vertex's parent (round 5; BfsWorkspace::pcode, one byte per vertex): the parent is
+// the vertex's first row entry (top1), its 2nd / 3rd / 4th (rest .x / .y / .z) -- the entries the pull kernel
+// probed first, which top1 / rest already hold -- or the explicit 4-B parent in par (a row walk, the push half of
+// a hybrid level, the encoded hub domain).  A discovery thus writes one byte where it wrote a 4-B parent; the
+// result's resolution reads the parent back from top1 / rest (or, in original ids, from otop1 / orest).
+constexpr uint8_t kCodeTop1 = 0, kCodeExplicit = 4;
+struct ParSrc {
+    const uint32_t *par;   // explicit parents
+    const uint8_t *code;   // provenance codes
+    const uint32_t *top1;  // first row entry (flag bits in fmask)
+    const uint4 *rest;     // 2nd..4th row entries (+ degree)
+    uint32_t fmask;
+};
+inline ParSrc par_src(const BfsWorkspace *ws) { return ParSrc{ws->par, ws->pcode, ws->top1, ws->rest, ws->top1_flag}; }
+__device__ __forceinline__ uint32_t record_parent(const ParSrc &ps, int64_t v) {
+    if (!ps.code) return ps.par[v]; // a partition's pull levels store every parent explicitly
+    const uint8_t c = ps.code[v];
+    if (c == kCodeTop1) return ps.top1[v] & ~ps.fmask;
+    if (c < kCodeExplicit) {
+        const uint4 r = ps.rest[v];
+        return c == 1 ? r.x : c == 2 ? r.y : r.z;
+    }
+    return ps.par[v];
+}
+
+// state of internal vertex i: st[i], unless a record holds i (its parent is then recorded by ps).  Lanes of
+// consecutive i share their record words (one broadcast load per wave and record).
+__device__ __forceinline__ u64 rec_state(const u64 *__restrict__ stt, const ParSrc &ps, const RecSet &rs, int64_t i) {
     for (int r = 0; r < rs.n; r++)
-        if ((rs.bm[r][i >> 6] >> (i & 63)) & 1ull) return pack_state(par[i], rs.nd[r]);
+        if ((rs.bm[r][i >> 6] >> (i & 63)) & 1ull) return pack_state(record_parent(ps, i), rs.nd[r]);
     return stt[i];
 }
 
@@ -902,8 +934,7 @@ __global__ __launch_bounds__(kBS) void k_resolve_log(const u64 *__restrict__ plo
 // st[v] = (par[v], nd_r) for every vertex v of every record r (the validator's and m_comp's view of a result;
 // a BFS with more than kMaxRec pull levels).  One wave per bitmap word, lane = bit: a word's par loads and state
 // stores are one coalesced access each.
-__global__ __launch_bounds__(kBS) void k_resolve(RecSet rs, int64_t nwords, const uint32_t *__restrict__ par,
-                                                 u64 *__restrict__ stt) {
+__global__ __launch_bounds__(kBS) void k_resolve(RecSet rs, int64_t nwords, ParSrc ps, u64 *__restrict__ stt) {
     const unsigned lane = lane_id();
     const int64_t nwaves = ((int64_t)gridDim.x * kBS) >> 6;
     for (int64_t w = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; w < nwords; w += nwaves) {
@@ -912,7 +943,7 @@ __global__ __launch_bounds__(kBS) void k_resolve(RecSet rs, int64_t nwords, cons
             if (m == 0ull) continue; // wave-uniform
             if ((m >> lane) & 1ull) {
                 const int64_t v = w * 64 + lane;
-                stt[v] = pack_state(par[v], rs.nd[r]);
+                stt[v] = pack_state(record_parent(ps, v), rs.nd[r]);
             }
         }
     }
@@ -947,7 +978,7 @@ struct RecLog {
         hipStream_t st = g->ctx->stream;
         if (n == kMaxRec) {
             hipLaunchKernelGGL(k_resolve, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st,
-                               set(), ws->nwords, ws->par, ws->st);
+                               set(), ws->nwords, par_src(ws), ws->st);
             BFSX_LAUNCHED(st);
             n = 0;
         }

@@ -437,6 +437,12 @@ static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "persist must be on|off");
         return BFSX_OK;
     }
+    if (k == "hub_lds_skip") {
+        if (v == "on") ctx->opt.hub_lds_skip = true;
+        else if (v == "off") ctx->opt.hub_lds_skip = false;
+        else return fail(BFSX_E_ARG, "hub_lds_skip must be on|off");
+        return BFSX_OK;
+    }
     if (k == "push_log") {
         if (v == "on") ctx->opt.push_log = true;
         else if (v == "off") ctx->opt.push_log = false;

@@ -40,6 +40,7 @@ struct Options {
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
     bool push_log = true;       // single device: per-level push winners go to the push log, not the packed state
+    bool hub_lds_skip = true;   // single device: the hub bin skips targets an LDS snapshot of the hubs' visited bits marks
     int persist_blocks = 0;     // K3p workgroups (0: auto, three per four CUs)
     int offset_bits = 0;        // traversal row-offset width: 0 = uint32 when nnz < 2^32, else int64; 64 = int64
     bool degree_order = true;   // rows ordered by neighbour degree (desc) instead of id (asc)

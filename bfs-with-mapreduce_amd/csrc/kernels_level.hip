@@ -17,13 +17,12 @@ namespace {
 // the unreached word the buffer was filled with once, except keep0 / keep1 (this BFS's source, the last one
 // written that was isolated), so only the other half costs a scattered store.
 template <bool kRelabel>
-__global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, const uint32_t *__restrict__ par,
-                                                RecSet rs, const uint32_t *__restrict__ inv, int64_t lo, int64_t n,
+__global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, ParSrc ps, RecSet rs, const uint32_t *__restrict__ inv, int64_t lo, int64_t n,
                                                 const u64 *__restrict__ dead, int64_t keep0, int64_t keep1,
                                                 u64 *__restrict__ out, int32_t *__restrict__ dist_only) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
         if (((dead[i >> 6] >> (i & 63)) & 1ull) && i != keep0 && i != keep1) continue;
-        const u64 s = rec_state(stt, par, rs, i);
+        const u64 s = rec_state(stt, ps, rs, i);
         const uint32_t o = kRelabel ? (uint32_t)((int64_t)inv[lo + i] - lo) : (uint32_t)i;
         if (dist_only) {
             dist_only[o] = (int32_t)(uint32_t)s;
@@ -38,61 +37,100 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, con
 // The result in ORIGINAL id order (a relabelled graph), in two passes (round 5; round 4 ran one gather of
 // 0.685 ms per scale-26 result whose every entry chained perm -> dead word -> one record word per pull level ->
 // st or par -> inv, each a dependent gather):
-//   phase 1, k_resolve_all, INTERNAL id order: one wave per 64-vertex bitmap word, lane = bit.  The word's record
-//     words are broadcast loads issued together; par, st and tmp are coalesced.  A record vertex's state
-//     (par[i], the record's distance) is stored into st, so st ends resolved (parents in internal ids: the
-//     Graph500 kernel-2 result on the device, which the validator and m_comp read), and with tmp every live i
-//     gets tmp[i] = parent_original << 32 | dist, the parent mapped through inv here, where the parents of
-//     consecutive vertices are the same few hubs (inv lines stay cached).  Only the words below iso_lo (the
-//     isolated tail) and the source's word are visited.
+//   phase 1, k_unpack_live, INTERNAL id order over the live ids (below iso_lo, the isolated tail): tmp[i] =
+//     parent_original << 32 | dist.  A record vertex (found by a pull level) takes its distance from the record
+//     and its parent from its provenance code (ParSrc): codes 0-3 read the original-id copy of the row entry
+//     the pull kernel probed (otop1 / orest, coalesced with i), code 4 the explicit parent through inv.  Other
+//     vertices read st, their parent through inv.  The record words are broadcast loads (a wave's 64 lanes share
+//     one), everything else coalesced except the inv lookups of push-found vertices.  st is left as it is: the
+//     validator and m_comp fold the records into it when they run (bfs_resolve).
 //   phase 2, k_unpack_gather: thread o reads perm[o] and copies tmp[perm[o]] into out[o] -- whole-line writes,
 //     near-sequential reads (the relabel keeps original order inside a degree class) -- or writes the unreached
 //     word without a load for an id of the isolated tail.
-constexpr int kResolveWords = 4; // bitmap words (of 64 vertices) one wave resolves per step, their loads issued together
+// Both passes are streams with one dependent gather per element; a grid-stride loop with one element per
+// iteration leaves them latency-bound (each wave waits a whole memory round trip per element: 0.35 + 0.30 ms at
+// scale 26 in a rocprof trace, against ~0.15 ms each at the streaming rate).  So every thread handles kUnpackU
+// elements per step -- tiles of kBS * kUnpackU consecutive ids per workgroup, every load of a stage issued
+// before the first is used.
+constexpr int kUnpackU = 8;
 
-__global__ __launch_bounds__(kBS) void k_resolve_all(RecSet rs, int64_t nwords_live, int64_t src_word,
-                                                     const uint32_t *__restrict__ par, u64 *__restrict__ stt,
+// otop1[v] / orest[v]: top1 / rest with their entries mapped to original ids (built once per graph, at its first
+// unpack; the degree-1 flag of top1 dropped)
+__global__ __launch_bounds__(kBS) void k_orig_nbrs(const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
+                                                   uint32_t fmask, const uint32_t *__restrict__ inv, int64_t n,
+                                                   uint32_t *__restrict__ otop1, uint4 *__restrict__ orest) {
+    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < n; v += (int64_t)gridDim.x * kBS) {
+        otop1[v] = inv[top1[v] & ~fmask];
+        const uint4 r = rest[v];
+        orest[v] = make_uint4(inv[r.x], inv[r.y], inv[r.z], r.w);
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_unpack_live(RecSet rs, int64_t live_n, int64_t src, ParSrc ps,
+                                                     const uint32_t *__restrict__ otop1,
+                                                     const uint4 *__restrict__ orest, const u64 *__restrict__ stt,
                                                      const uint32_t *__restrict__ inv, u64 *__restrict__ tmp,
                                                      int64_t n) {
-    const unsigned lane = lane_id();
-    const int64_t nwaves = ((int64_t)gridDim.x * kBS) >> 6;
-    const int64_t ngroups = (nwords_live + kResolveWords - 1) / kResolveWords;
-    const int64_t nit = ngroups + (src_word >= nwords_live ? 1 : 0); // + the isolated source's word alone
-    for (int64_t it = ((int64_t)blockIdx.x * kBS + threadIdx.x) >> 6; it < nit; it += nwaves) {
-        const int64_t wb = it < ngroups ? it * kResolveWords : src_word;
-        const int64_t nw = it < ngroups ? std::min<int64_t>(kResolveWords, nwords_live - wb) : 1;
-        int hit[kResolveWords];
+    constexpr int64_t kTile = (int64_t)kBS * kUnpackU;
+    for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < live_n; t0 += (int64_t)gridDim.x * kTile) {
+        int hit[kUnpackU];
 #pragma unroll
-        for (int j = 0; j < kResolveWords; j++) hit[j] = -1;
-        for (int r = 0; r < rs.n; r++) { // records are disjoint: every word's load is independent
+        for (int j = 0; j < kUnpackU; j++) hit[j] = -1;
+        for (int r = 0; r < rs.n; r++) { // records are disjoint; a wave's 64 lanes share each word (broadcast)
 #pragma unroll
-            for (int j = 0; j < kResolveWords; j++)
-                if (j < nw && ((rs.bm[r][wb + j] >> lane) & 1ull)) hit[j] = r;
+            for (int j = 0; j < kUnpackU; j++) {
+                const int64_t v = t0 + j * kBS + threadIdx.x;
+                if (v < live_n && ((rs.bm[r][v >> 6] >> (v & 63)) & 1ull)) hit[j] = r;
+            }
         }
-        u64 s[kResolveWords];
+        uint32_t code[kUnpackU];
 #pragma unroll
-        for (int j = 0; j < kResolveWords; j++) {
-            const int64_t v = (wb + j) * 64 + lane;
-            s[j] = kUnreached;
-            if (j < nw && v < n) s[j] = hit[j] >= 0 ? pack_state(par[v], rs.nd[hit[j]]) : stt[v];
+        for (int j = 0; j < kUnpackU; j++) {
+            const int64_t v = t0 + j * kBS + threadIdx.x;
+            code[j] = (v < live_n && hit[j] >= 0) ? ps.code[v] : 0xFFu;
+        }
+        // the internal parent (explicit, or st's) that still needs inv; or the original parent directly
+        uint32_t p[kUnpackU], d[kUnpackU];
+        bool mapped[kUnpackU];
+#pragma unroll
+        for (int j = 0; j < kUnpackU; j++) {
+            const int64_t v = t0 + j * kBS + threadIdx.x;
+            mapped[j] = false;
+            p[j] = 0xFFFFFFFFu;
+            d[j] = (uint32_t)INT32_MAX;
+            if (v >= live_n) continue;
+            if (hit[j] < 0) {
+                const u64 s = stt[v];
+                p[j] = (uint32_t)(s >> 32);
+                d[j] = (uint32_t)s;
+                continue;
+            }
+            d[j] = (uint32_t)rs.nd[hit[j]];
+            const uint32_t c = code[j];
+            if (otop1 && c == kCodeTop1) {
+                p[j] = otop1[v];
+                mapped[j] = true;
+            } else if (otop1 && c < kCodeExplicit) {
+                const uint4 r = orest[v];
+                p[j] = c == 1 ? r.x : c == 2 ? r.y : r.z;
+                mapped[j] = true;
+            } else {
+                p[j] = record_parent(ps, v);
+            }
         }
 #pragma unroll
-        for (int j = 0; j < kResolveWords; j++) {
-            const int64_t v = (wb + j) * 64 + lane;
-            if (j < nw && v < n && hit[j] >= 0) stt[v] = s[j];
-        }
-        if (!tmp) continue;
-        uint32_t po[kResolveWords];
+        for (int j = 0; j < kUnpackU; j++)
+            if (!mapped[j] && p[j] != 0xFFFFFFFFu) p[j] = inv[p[j]];
 #pragma unroll
-        for (int j = 0; j < kResolveWords; j++) {
-            const uint32_t p = (uint32_t)(s[j] >> 32);
-            po[j] = (j < nw && p != 0xFFFFFFFFu) ? inv[p] : p;
+        for (int j = 0; j < kUnpackU; j++) {
+            const int64_t v = t0 + j * kBS + threadIdx.x;
+            if (v < live_n) tmp[v] = ((u64)p[j] << 32) | d[j];
         }
-#pragma unroll
-        for (int j = 0; j < kResolveWords; j++) {
-            const int64_t v = (wb + j) * 64 + lane;
-            if (j < nw && v < n) tmp[v] = ((u64)po[j] << 32) | (uint32_t)s[j];
-        }
+    }
+    // an isolated source lies in the tail the loop skips: its state (distance 0, itself as parent) is in st
+    if (src >= live_n && src < n && blockIdx.x == 0 && threadIdx.x == 0) {
+        const u64 s = stt[src];
+        tmp[src] = ((u64)inv[(uint32_t)(s >> 32)] << 32) | (uint32_t)s;
     }
 }
 
@@ -103,14 +141,27 @@ constexpr int kXcds = 8;
 __global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ tmp, const uint32_t *__restrict__ perm,
                                                        int64_t n, int64_t iso_lo, int64_t src, u64 *__restrict__ out,
                                                        int32_t *__restrict__ dist_only) {
+    constexpr int64_t kTile = (int64_t)kBS * kUnpackU;
     const int64_t per_xcd = (n + kXcds - 1) / kXcds;
     const int64_t lo = (int64_t)(blockIdx.x % kXcds) * per_xcd, hi = std::min<int64_t>(lo + per_xcd, n);
-    const int64_t step = (int64_t)(gridDim.x / kXcds) * kBS;
-    for (int64_t o = lo + (int64_t)(blockIdx.x / kXcds) * kBS + threadIdx.x; o < hi; o += step) {
-        const int64_t i = (int64_t)perm[o];
-        const u64 s = (i >= iso_lo && i != src) ? kUnreached : tmp[i];
-        if (dist_only) dist_only[o] = (int32_t)(uint32_t)s;
-        else out[o] = s;
+    const int64_t step = (int64_t)(gridDim.x / kXcds) * kTile;
+    for (int64_t t0 = lo + (int64_t)(blockIdx.x / kXcds) * kTile; t0 < hi; t0 += step) {
+        int64_t i[kUnpackU];
+#pragma unroll
+        for (int j = 0; j < kUnpackU; j++) {
+            const int64_t o = t0 + j * kBS + threadIdx.x;
+            i[j] = o < hi ? (int64_t)perm[o] : iso_lo;
+        }
+        u64 s[kUnpackU];
+#pragma unroll
+        for (int j = 0; j < kUnpackU; j++) s[j] = (i[j] < iso_lo || i[j] == src) ? tmp[i[j]] : kUnreached;
+#pragma unroll
+        for (int j = 0; j < kUnpackU; j++) {
+            const int64_t o = t0 + j * kBS + threadIdx.x;
+            if (o >= hi) continue;
+            if (dist_only) dist_only[o] = (int32_t)(uint32_t)s[j];
+            else out[o] = s[j];
+        }
     }
 }
 
@@ -209,11 +260,22 @@ __global__ __launch_bounds__(kBS) void k_popc(const u64 *__restrict__ bm, int64_
 __global__ __launch_bounds__(kBS) void k_mcomp(const u64 *__restrict__ stt, const uint32_t *__restrict__ tcnt,
                                                int64_t nv, u64 *out) {
     u64 m = 0, r = 0;
-    for (int64_t v = (int64_t)blockIdx.x * kBS + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBS) {
-        if ((int32_t)(uint32_t)stt[v] != INT32_MAX) {
-            m += tcnt[v];
-            r += 1;
+    constexpr int kU = 8; // loads in flight per thread (a one-element grid-stride loop was latency-bound: 325 us)
+    for (int64_t t0 = (int64_t)blockIdx.x * kBS * kU; t0 < nv; t0 += (int64_t)gridDim.x * kBS * kU) {
+        u64 s[kU];
+        uint32_t c[kU];
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+            const int64_t v = t0 + j * kBS + threadIdx.x;
+            s[j] = v < nv ? stt[v] : (u64)INT32_MAX;
+            c[j] = v < nv ? tcnt[v] : 0u;
         }
+#pragma unroll
+        for (int j = 0; j < kU; j++)
+            if ((int32_t)(uint32_t)s[j] != INT32_MAX) {
+                m += c[j];
+                r += 1;
+            }
     }
     m = wave_sum(m);
     r = wave_sum(r);
@@ -375,6 +437,7 @@ int ws_alloc(bfsx_graph *g) {
     const size_t nv = (size_t)std::max<int64_t>(g->nv, 1);
     BFSX_HIP_TRY(hipMalloc(&ws->st, nv * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->par, nv * sizeof(uint32_t)));
+    if (g->nranks == 1) BFSX_HIP_TRY(hipMalloc(&ws->pcode, nv));
     BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(u64)));
@@ -525,7 +588,8 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
-                    (void *)ws->d_dist_ctr, (void *)ws->out64, (void *)ws->rtmp})
+                    (void *)ws->d_dist_ctr, (void *)ws->out64, (void *)ws->rtmp, (void *)ws->pcode, (void *)ws->otop1,
+                    (void *)ws->orest})
         if (p) (void)hipFree(p);
     for (const auto &r : ws->retired) (void)hipFree(const_cast<void *>(r.p));
     for (void *p : ws->prec) (void)hipFree(p);
@@ -982,7 +1046,7 @@ int bfs_resolve(bfsx_graph *g) {
         rs.nd[r] = ws->prec_nd[r];
     }
     hipLaunchKernelGGL(k_resolve, dim3(clamp_grid((ws->nwords * 64 + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, rs,
-                       ws->nwords, ws->par, ws->st);
+                       ws->nwords, par_src(ws), ws->st);
     BFSX_LAUNCHED(st);
     ws->resolved = true;
     return BFSX_OK;
@@ -1074,6 +1138,21 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         BFSX_HIP_TRY(hipStreamSynchronize(st));
         src_dead = (dw >> (src & 63)) & 1ull;
     }
+    if (gather && !ws->orig_nbrs_tried) { // once per graph, outside the unpack's time
+        ws->orig_nbrs_tried = true;
+        // not for the encoded hub domain, whose top1 / rest are not vertex ids (its pull parents are all explicit)
+        if (ws->hub_k == 0 && ws->pcode && hipMalloc(&ws->otop1, nv * sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc(&ws->orest, nv * sizeof(uint4)) == hipSuccess) {
+            hipLaunchKernelGGL(k_orig_nbrs, grid, dim3(kBS), 0, st, ws->top1, ws->rest, ws->top1_flag, g->d_inv,
+                               (int64_t)nv, ws->otop1, ws->orest);
+            BFSX_LAUNCHED(st);
+        } else { // no room: codes 0-3 map through inv like explicit parents
+            (void)hipGetLastError();
+            if (ws->otop1) (void)hipFree(ws->otop1);
+            ws->otop1 = nullptr;
+            ws->orest = nullptr;
+        }
+    }
     if (int e = apply_logs(g, ws, ws->ev_unpack0)) return e; // the push log is part of the unpack's time
     if (gather) {
         u64 *tmp = ws->plog; // free once the log is scattered (apply_logs above)
@@ -1081,23 +1160,23 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
             if (!ws->rtmp) BFSX_HIP_TRY(hipMalloc(&ws->rtmp, std::max<size_t>(nv, 1) * sizeof(u64)));
             tmp = ws->rtmp;
         }
-        const int64_t nw_live = std::min<int64_t>((ws->iso_lo + 63) / 64, ws->nwords);
-        const int64_t src_word = src >= 0 ? src / 64 : 0;
-        const int64_t groups = (nw_live + kResolveWords - 1) / kResolveWords + 1;
-        hipLaunchKernelGGL(k_resolve_all, dim3(clamp_grid((groups + kWaves - 1) / kWaves, 8192)), dim3(kBS), 0, st,
-                           rs, nw_live, src_word, ws->par, ws->st, g->d_inv, tmp, (int64_t)nv);
+        const int64_t live_n = std::min<int64_t>(ws->iso_lo, (int64_t)nv);
+        const int64_t tile = (int64_t)kBS * kUnpackU;
+        hipLaunchKernelGGL(k_unpack_live, dim3(clamp_grid((live_n + tile - 1) / tile, 4096)), dim3(kBS), 0, st,
+                           rs, live_n, src, par_src(ws), ws->otop1, ws->orest, ws->st, g->d_inv, tmp, (int64_t)nv);
         BFSX_LAUNCHED(st);
-        ws->resolved = true; // st now holds every record vertex's state too (bfs_resolve has nothing left to do)
         BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack_mid, st));
-        const unsigned gx = std::max<unsigned>(kXcds, grid.x / kXcds * kXcds); // a multiple of the XCD count
+        // a multiple of the XCD count, about one tile per workgroup
+        const unsigned gx = std::max<unsigned>(
+            kXcds, clamp_grid(((int64_t)nv + (int64_t)kBS * kUnpackU - 1) / ((int64_t)kBS * kUnpackU), 4096) / kXcds * kXcds);
         hipLaunchKernelGGL(k_unpack_gather, dim3(gx), dim3(kBS), 0, st, tmp, g->d_perm, (int64_t)nv, ws->iso_lo, src,
                            ws->out64, d_dist_only);
         ws->out_mode = 0; // every entry written: a later scatter-mode unpack must prefill again
     } else if (g->d_inv)
-        hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo, (int64_t)nv,
+        hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, par_src(ws), rs, g->d_inv, g->v_lo, (int64_t)nv,
                            ws->dead, src, ws->out_dirty, ws->out64, d_dist_only);
     else
-        hipLaunchKernelGGL(k_unpack<false>, grid, dim3(kBS), 0, st, ws->st, ws->par, rs, g->d_inv, g->v_lo,
+        hipLaunchKernelGGL(k_unpack<false>, grid, dim3(kBS), 0, st, ws->st, par_src(ws), rs, g->d_inv, g->v_lo,
                            (int64_t)nv, ws->dead, src, ws->out_dirty, ws->out64, d_dist_only);
     BFSX_LAUNCHED(st);
     ws->out_dirty = src_dead ? src : -1;

@@ -106,12 +106,18 @@ constexpr uint32_t kBuCand = 64u * 64u / (uint32_t)kBuParts;
 struct PrefixSpec {
     uint32_t ids, nseg, shift, pad;
 };
-// A pull level's discovery: the 4-B parent only (the level's record bitmap gives the distance, BfsWorkspace::par;
-// one device and the partitioned loop alike); par_out == null: the packed state.
-__device__ __forceinline__ void settle_state(u64 *__restrict__ stt, uint32_t *__restrict__ par_out, uint32_t v,
+// A pull level's discovery: its provenance code, plus the 4-B parent when the code is explicit (the level's record
+// bitmap gives the distance; BfsWorkspace::pcode / par, one device and the partitioned loop alike); par_out ==
+// null: the packed state (the test suite's level primitives).
+__device__ __forceinline__ void settle_state(u64 *__restrict__ stt, uint32_t *__restrict__ par_out,
+                                             uint8_t *__restrict__ code_out, uint32_t v, uint32_t code,
                                              uint32_t parent, int32_t nd) {
-    if (par_out) par_out[v] = parent;
-    else stt[v] = pack_state(parent, nd);
+    if (par_out) {
+        if (code_out) code_out[v] = (uint8_t)code;
+        if (!code_out || code == kCodeExplicit) par_out[v] = parent;
+    } else {
+        stt[v] = pack_state(parent, nd);
+    }
 }
 
 // kSpill: a diagnostic instantiation compiled for 8 waves per SIMD (64 VGPRs), so it spills to scratch --
@@ -121,7 +127,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
                                             u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out,
-                                            LevelSlot *ring, int level,
+                                            uint8_t *__restrict__ code_out, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
                                             const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo,
                                             PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim) {
@@ -256,12 +262,13 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                     const bool deg1 = (x[k] & fmask) != 0; // top1 was the row's only entry
                     const uint32_t deg = r[k].w;           // 0 unless A2 ran
                     bool found = false, miss = false;
-                    uint32_t par = 0;
+                    uint32_t par = 0, code = kCodeExplicit; // the encoded hub domain names every parent explicitly
                     const uint32_t pb = (pbm >> (3 * k)) & 7u;
                     if (ok) {
                         if ((fbm >> k) & 1u) {
                             found = true;
                             par = x[k] & ~fmask;
+                            if (!kHubs) code = kCodeTop1;
                             acc_sc += 1;
                         } else if (deg1) {
                             acc_mu += 1;
@@ -272,6 +279,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         } else if (pb) {
                             found = true;
                             par = (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z;
+                            if (!kHubs) code = (uint32_t)__ffs((int)pb); // 1, 2, 3: rest .x, .y, .z
                             acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
                         } else if (deg <= 4u || (kHubOnly && !(hub_entry<kHubs>(r[k].x, hub_lim) &&
                                                                hub_entry<kHubs>(r[k].y, hub_lim) &&
@@ -284,7 +292,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         }
                     }
                     if (found) {
-                        settle_state(stt, par_out, v[k], probe_id<kHubs>(hub_id, par), nd);
+                        settle_state(stt, par_out, code_out, v[k], code, probe_id<kHubs>(hub_id, par), nd);
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
                         if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
@@ -344,7 +352,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         acc_wk += (uint32_t)(j - b - 4);
                         acc_rows += 1;
                         if (found) {
-                            settle_state(stt, par_out, vv, probe_id<kHubs>(hub_id, par), nd);
+                            settle_state(stt, par_out, code_out, vv, kCodeExplicit, probe_id<kHubs>(hub_id, par), nd);
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
                             if (kMf) acc_mf += (uint32_t)(e - b);
@@ -378,12 +386,14 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
 #define BFSX_K_BU_PARAMS                                                                                        \
     const OffT *__restrict__ row_off, const uint32_t *__restrict__ col, const uint32_t *__restrict__ top1,      \
         const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next,                  \
-        u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out, LevelSlot *ring, int level,   \
+        u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out, uint8_t *__restrict__ code_out, \
+        LevelSlot *ring, int level,                                                                            \
         int64_t nwords, uint32_t fmask,                                                                        \
         const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo, \
         PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim
 #define BFSX_K_BU_ARGS                                                                                          \
-    row_off, col, top1, rest, front, next, vis, stt, par_out, ring, level, nwords, fmask, hfront, hub_id, hub_lim,     \
+    row_off, col, top1, rest, front, next, vis, stt, par_out, code_out, ring, level, nwords, fmask, hfront, hub_id,    \
+        hub_lim,                                                                                               \
         leaf_lo, pf,                                                                                           \
         pub, seq, hub_row_lim
 
@@ -420,7 +430,8 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
                                                    const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                                    const u64 *__restrict__ front, u64 *__restrict__ next,
                                                    u64 *__restrict__ vis, u64 *__restrict__ stt,
-                                                   uint32_t *__restrict__ par_out, LevelSlot *ring,
+                                                   uint32_t *__restrict__ par_out, uint8_t *__restrict__ code_out,
+                                                   LevelSlot *ring,
                                                    int level, int64_t nwords, uint32_t fmask, uint32_t hub_row_lim,
                                                    uint32_t qlim, uint32_t *__restrict__ qout, Published *pub,
                                                    u64 seq) {
@@ -437,9 +448,9 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
     auto fbit = [&](uint32_t x) -> uint32_t { return (front32[x >> 5] >> (x & 31u)) & 1u; };
     int64_t wb = 0; // first word of the wave's current range
     // state word + next-frontier bit of a found vertex; wave-uniform queue append of the ones below qlim
-    auto settle = [&](bool found, uint32_t v, uint32_t par) {
+    auto settle = [&](bool found, uint32_t v, uint32_t code, uint32_t par) {
         if (found) {
-            settle_state(stt, par_out, v, par, nd);
+            settle_state(stt, par_out, code_out, v, code, par, nd);
             atomicOr(&s_nx[wave][(int64_t)(v >> 6) - wb], 1ull << (v & 63u));
             acc_nf += 1;
             acc_nh += v < hub_row_lim ? 1u : 0u;
@@ -484,12 +495,13 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             bool found = false, miss = false;
-            uint32_t par = 0;
+            uint32_t par = 0, code = kCodeExplicit;
             const uint32_t pb = (pbm >> (3 * k)) & 7u, deg = r[k].w;
             if (ok[k]) {
                 if ((fbm >> k) & 1u) {
                     found = true;
                     par = x[k] & ~fmask;
+                    code = kCodeTop1;
                     acc_sc += 1;
                 } else if (x[k] & fmask) { // top1 was the row's only entry
                     acc_mu += 1;
@@ -497,6 +509,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
                 } else if (pb) {
                     found = true;
                     par = (pb & 1u) ? r[k].x : (pb & 2u) ? r[k].y : r[k].z;
+                    code = (uint32_t)__ffs((int)pb);
                     acc_sc += 2u + (uint32_t)__ffs((int)pb) - 1u;
                 } else if (deg <= 4u) {
                     acc_mu += deg;
@@ -506,7 +519,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
                     acc_sc += 4;
                 }
             }
-            settle(found, v[k], par);
+            settle(found, v[k], code, par);
             const u64 mm = __ballot(miss);
             if (miss) s_miss[wave][nmiss + __popcll(mm & ((1ull << lane) - 1ull))] = v[k];
             nmiss += (uint32_t)__popcll(mm);
@@ -541,7 +554,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
                 acc_rows += 1;
                 if (!found) acc_mu += (uint32_t)(e - b);
             }
-            settle(found, vv, par);
+            settle(found, vv, kCodeExplicit, par);
         }
         __builtin_amdgcn_wave_barrier();
     };
@@ -663,7 +676,8 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
 #endif
 #define BFSX_K_BU_LAUNCH(kern)                                                                                   \
     hipLaunchKernelGGL(kern, grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, \
-                       next, ws->vis, ws->st, par, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront, ws->hub_id,  \
+                       next, ws->vis, ws->st, par, ws->pcode, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront,  \
+                       ws->hub_id,                                                                                      \
                        ws->hub_lim, (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws),  \
                        pub, seq, (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll))
 #ifdef BFSX_DIAG
@@ -729,11 +743,13 @@ int launch_bu_sparse(bfsx_graph *g, BfsWorkspace *ws, const u64 *front, u64 *nex
     const uint32_t hrl = (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll);
     if (ws->off32)
         hipLaunchKernelGGL(k_bu_sparse<uint32_t>, grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->top1, ws->rest,
-                           front, next, ws->vis, ws->st, par, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
+                           front, next, ws->vis, ws->st, par, ws->pcode, ws->ring, level, ws->nwords, ws->top1_flag, hrl,
+                           qlim,
                            ws->qa, pub, seq);
     else
         hipLaunchKernelGGL(k_bu_sparse<int64_t>, grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->top1, ws->rest,
-                           front, next, ws->vis, ws->st, par, ws->ring, level, ws->nwords, ws->top1_flag, hrl, qlim,
+                           front, next, ws->vis, ws->st, par, ws->pcode, ws->ring, level, ws->nwords, ws->top1_flag, hrl,
+                           qlim,
                            ws->qa, pub, seq);
     BFSX_LAUNCHED(st);
     return BFSX_OK;

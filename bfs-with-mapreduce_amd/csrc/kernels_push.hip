@@ -8,17 +8,24 @@ namespace bfsx {
 
 namespace {
 
+constexpr uint32_t kVisPref = 1u << 16; // ids whose visited bits the hub bin snapshots into LDS (8 KiB)
+
 // Sweep edges [x_begin, x_end) of a segment table (scan/beg/u in LDS, n entries; u = local row id)
 // in steps of kBS*kItems.  Block-uniform.  kDist: targets owned by another rank become remote pairs.
 // par != null (the push half of a hybrid level): a winner's parent also goes to the 4-B parent array, because the
-// level's discoveries are merged into the pull half's level record, whose vertices take their parent from there.
+// level's discoveries are merged into the pull half's level record, whose vertices take their parent from there
+// (provenance code kCodeExplicit in pcode).
+// s_vp / vpref (the hub bin of a relabelled single-device graph, option hub_lds_skip): the visited bits of ids below
+// vpref as they stood when the level began, in LDS.  A target whose bit is set there needs no global probe -- on the
+// hub-core level most edges of a degree-ordered hub row start with other hubs, visited a level earlier.
 template <bool kDist, class OffT, class ScanT, class Q>
 __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
-                                      uint32_t *__restrict__ par, int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
+                                      uint32_t *__restrict__ par, uint8_t *__restrict__ pcode, int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
-                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh, u64 *__restrict__ plog) {
+                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh, u64 *__restrict__ plog,
+                                      const u64 *s_vp = nullptr, uint32_t vpref = 0u) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
         bool valid[kItems];
@@ -47,11 +54,15 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                 send = valid[k] && (v[k] / pt.chunk) != pt.rank;
                 vl = v[k] - pt.lo;
             }
-            if (valid[k] && !send && claim(vl, vis, attempts)) {
+            const bool known = vpref && vl < vpref && ((s_vp[vl >> 6] >> (vl & 63u)) & 1ull);
+            if (valid[k] && !send && !known && claim(vl, vis, attempts)) {
                 win = true;
                 // the push log (single device) or the hybrid level's parent array + record carry the result;
                 // else the packed state
-                if (par) par[vl] = pu[k];
+                if (par) {
+                    par[vl] = pu[k];
+                    if (pcode) pcode[vl] = kCodeExplicit;
+                }
                 else if (!plog) stt[vl] = pack_state(pu[k], nd);
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
                 acc_mf += dg;
@@ -74,7 +85,8 @@ template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ qin, uint32_t qlen,
                                             uint32_t *__restrict__ qout, u64 *vis, u64 *__restrict__ stt,
-                                            uint32_t *__restrict__ par, LevelSlot *ring, int level, uint32_t hub_deg,
+                                            uint32_t *__restrict__ par, uint8_t *__restrict__ pcode, LevelSlot *ring,
+                                            int level, uint32_t hub_deg,
                                             uint32_t *__restrict__ hubs, Part pt, int gsz, HubSet hs,
                                             HubSet skip, Published *pub, u64 seq, u64 *__restrict__ plog) {
     LevelSlot *cn = ring + (level + 1) % 3;
@@ -132,8 +144,8 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             scanned += total;
         }
         __syncthreads();
-        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, par, nd, q, qout, &cn->qtail, pt, rq,
-                              acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog);
+        sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, par, pcode, nd, q, qout, &cn->qtail, pt,
+                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog);
         __syncthreads();
     }
     q_flush(q, qout, plog, &cn->qtail);
@@ -148,9 +160,19 @@ template <bool kDist, class OffT>
 __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                                  const uint32_t *__restrict__ hubs, uint32_t *__restrict__ qout,
                                                  u64 *vis, u64 *__restrict__ stt, uint32_t *__restrict__ par,
-                                                 LevelSlot *ring, int level,
-                                                 Part pt, HubSet hs, Published *pub, u64 seq, u64 *__restrict__ plog) {
+                                                 uint8_t *__restrict__ pcode, LevelSlot *ring, int level,
+                                                 Part pt, HubSet hs, Published *pub, u64 seq, u64 *__restrict__ plog,
+                                                 uint32_t vpref) {
     LevelSlot *cn = ring + (level + 1) % 3;
+    // single device: the level's starting visited bits of the ids below vpref (hub_lds_skip); 8 KiB of LDS
+    __shared__ typename std::conditional<kDist, char, u64[kVisPref / 64]>::type s_vp_storage;
+    const u64 *s_vp = nullptr;
+    if constexpr (!kDist) {
+        for (uint32_t w = threadIdx.x; w < vpref / 64u; w += kBS) s_vp_storage[w] = vis[w];
+        s_vp = s_vp_storage;
+    } else {
+        vpref = 0u;
+    }
     __shared__ u64 s_scan[kHubBatch + 1];
     __shared__ int64_t s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
@@ -206,8 +228,8 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
-        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, par, nd, q, qout, &cn->qtail, pt,
-                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog);
+        sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, par, pcode, nd, q, qout,
+                              &cn->qtail, pt, rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog, s_vp, vpref);
         __syncthreads();
     }
     q_flush(q, qout, plog, &cn->qtail);
@@ -230,6 +252,7 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
               bool skip_hubs, Published *pub, u64 seq, uint32_t *par,
               u64 *plog) {
     hipStream_t st = g->ctx->stream;
+    uint8_t *pcode = par ? ws->pcode : nullptr;
     const HubSet hs = hub_set(ws);
     const HubSet skip = skip_hubs ? hs : HubSet{0xFFFFFFFFu, 0u};
     const unsigned cap = (unsigned)g->ctx->num_cus * 8u;
@@ -243,24 +266,27 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     // slot mode: only the level's last push kernel writes the slot headers
     Part pt0 = pt;
     if (hubs) pt0.slot_arrive = nullptr;
+    // the LDS snapshot of the hubs' visited bits (relabelled single-device graphs: the hubs are the lowest ids)
+    const uint32_t vpref = (!kDist && g->d_perm && g->ctx->opt.hub_lds_skip)
+                               ? (uint32_t)std::min<int64_t>(kVisPref, ws->nwords * 64) : 0u;
     if (ws->off32) {
         hipLaunchKernelGGL((k_td<kDist, uint32_t>), grid, dim3(kBS), 0, st, ws->off32, g->d_col, ws->qa, (uint32_t)nf,
-                           ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
+                           ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
                            hubs ? nullptr : pub, seq, plog);
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq, plog);
+                               ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, pt, hs, pub, seq, plog, vpref);
             BFSX_LAUNCHED(st);
         }
     } else {
         hipLaunchKernelGGL((k_td<kDist, int64_t>), grid, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->qa,
-                           (uint32_t)nf, ws->qb, ws->vis, ws->st, par, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
+                           (uint32_t)nf, ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, hub_deg, ws->hubs, pt0, gsz, hs, skip,
                            hubs ? nullptr : pub, seq, plog);
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, par, ws->ring, level, pt, hs, pub, seq, plog);
+                               ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, pt, hs, pub, seq, plog, vpref);
             BFSX_LAUNCHED(st);
         }
     }

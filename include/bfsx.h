@@ -114,6 +114,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "push_log" = on|off (one device: a per-level push level writes its winners as (vertex, parent) pairs at
  *                 their queue positions instead of scattered state stores; the result read scatters them;
  *                 default on)
+ *   "hub_lds_skip" = on|off (single device, relabelled graphs: the multi-workgroup push bin reads the visited bits
+ *                 of the 2^16 highest-degree ids from an LDS snapshot taken at the level's start and probes no
+ *                 target that snapshot marks visited; default on)
  *   "persist_blocks" = auto|int (workgroups of that launch, auto = three per four CUs (192 on MI355X), capped
  *                 by the occupancy API so that every workgroup is resident; fixed at a graph's first BFS)
  *   "pull_min_edges" = int (a push -> pull switch also needs the frontier to hold at least this many edges,
