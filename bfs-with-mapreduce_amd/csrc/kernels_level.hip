@@ -72,50 +72,56 @@ __global__ __launch_bounds__(kBS) void k_unpack_live(RecSet rs, int64_t live_n, 
                                                      const uint32_t *__restrict__ inv, u64 *__restrict__ tmp,
                                                      int64_t n) {
     constexpr int64_t kTile = (int64_t)kBS * kUnpackU;
+    const unsigned lane = lane_id();
     for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < live_n; t0 += (int64_t)gridDim.x * kTile) {
+        // element j of a wave is one whole bitmap word: its record words are wave-uniform (scalar loads)
         int hit[kUnpackU];
 #pragma unroll
         for (int j = 0; j < kUnpackU; j++) hit[j] = -1;
-        for (int r = 0; r < rs.n; r++) { // records are disjoint; a wave's 64 lanes share each word (broadcast)
+        for (int r = 0; r < rs.n; r++) { // records are disjoint
+            const u64 *bm = rs.bm[r];
 #pragma unroll
             for (int j = 0; j < kUnpackU; j++) {
-                const int64_t v = t0 + j * kBS + threadIdx.x;
-                if (v < live_n && ((rs.bm[r][v >> 6] >> (v & 63)) & 1ull)) hit[j] = r;
+                const int wj = __builtin_amdgcn_readfirstlane((int)((t0 + j * kBS) >> 6) + (int)(threadIdx.x >> 6));
+                if ((int64_t)wj * 64 < live_n && ((bm[wj] >> lane) & 1ull)) hit[j] = r;
             }
         }
-        uint32_t code[kUnpackU];
+        // stage 1, issued together: a record vertex's code and the original id of its first row entry, anyone
+        // else's state
+        uint32_t code[kUnpackU], o1[kUnpackU];
+        u64 s[kUnpackU];
 #pragma unroll
         for (int j = 0; j < kUnpackU; j++) {
             const int64_t v = t0 + j * kBS + threadIdx.x;
-            code[j] = (v < live_n && hit[j] >= 0) ? ps.code[v] : 0xFFu;
+            const bool live = v < live_n;
+            code[j] = (live && hit[j] >= 0) ? ps.code[v] : 0xFFu;
+            o1[j] = (live && hit[j] >= 0 && otop1) ? otop1[v] : 0u;
+            s[j] = (live && hit[j] < 0) ? stt[v] : kUnreached;
         }
-        // the internal parent (explicit, or st's) that still needs inv; or the original parent directly
+        // stage 2: the parent of every other kind -- an original id already (codes 0-3 with the copies), or an
+        // internal id that goes through inv (explicit parents, st's)
         uint32_t p[kUnpackU], d[kUnpackU];
         bool mapped[kUnpackU];
 #pragma unroll
         for (int j = 0; j < kUnpackU; j++) {
             const int64_t v = t0 + j * kBS + threadIdx.x;
-            mapped[j] = false;
-            p[j] = 0xFFFFFFFFu;
-            d[j] = (uint32_t)INT32_MAX;
-            if (v >= live_n) continue;
-            if (hit[j] < 0) {
-                const u64 s = stt[v];
-                p[j] = (uint32_t)(s >> 32);
-                d[j] = (uint32_t)s;
-                continue;
-            }
-            d[j] = (uint32_t)rs.nd[hit[j]];
             const uint32_t c = code[j];
-            if (otop1 && c == kCodeTop1) {
-                p[j] = otop1[v];
-                mapped[j] = true;
-            } else if (otop1 && c < kCodeExplicit) {
-                const uint4 r = orest[v];
-                p[j] = c == 1 ? r.x : c == 2 ? r.y : r.z;
-                mapped[j] = true;
+            mapped[j] = false;
+            if (hit[j] < 0) {
+                p[j] = (uint32_t)(s[j] >> 32);
+                d[j] = (uint32_t)s[j];
             } else {
-                p[j] = record_parent(ps, v);
+                d[j] = (uint32_t)rs.nd[hit[j]];
+                if (otop1 && c == kCodeTop1) {
+                    p[j] = o1[j];
+                    mapped[j] = true;
+                } else if (otop1 && c < kCodeExplicit) {
+                    const uint4 r = orest[v];
+                    p[j] = c == 1 ? r.x : c == 2 ? r.y : r.z;
+                    mapped[j] = true;
+                } else {
+                    p[j] = record_parent(ps, v);
+                }
             }
         }
 #pragma unroll

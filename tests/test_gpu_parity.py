@@ -298,6 +298,47 @@ def test_push_log_matches_state_stores(ctx, persist):
         ctx.set_option("persist", "on")
 
 
+@pytest.mark.parametrize("relabel", ["on", "off"])
+@pytest.mark.parametrize("direction", ["auto", "bottomup"])
+def test_provenance_codes_every_reader(ctx, relabel, direction):
+    """Round 5: a pull level stores a 1-B provenance code per discovery (0: top1, 1-3: rest.x/y/z, 4: the
+    explicit 4-B parent) instead of the parent itself.  Every reader must decode it to the same tree: the unpack
+    read FIRST (k_unpack_live with the original-id copies of top1 / rest, relabel on; k_unpack's scatter form,
+    relabel off), then the device validator and m_comp (bfs_resolve folds the records into st lazily), then the
+    unpack again from the folded state.  A 160x160 grid pulled from level 0 has more than kMaxRec (32) pull levels,
+    so its records are folded mid-BFS (RecLog::take) as well."""
+    cases = []
+    u, v = O.kronecker(14, 16, 21)
+    cases.append((1 << 14, np.asarray(u, np.uint32), np.asarray(v, np.uint32)))
+    side = 160
+    idx = np.arange(side * side).reshape(side, side)
+    cases.append((side * side, np.r_[idx[:, :-1].ravel(), idx[:-1, :].ravel()].astype(np.uint32),
+                  np.r_[idx[:, 1:].ravel(), idx[1:, :].ravel()].astype(np.uint32)))
+    ctx.set_option("relabel", relabel)
+    ctx.set_option("direction", direction)
+    try:
+        for nv, u, v in cases:
+            off, col = O.build_sets(nv, u, v)
+            srcs = [int(u[0]), int(v[len(v) // 2]), int(u[-1])]
+            with ctx.from_edges(nv, u, v) as g:
+                for src in srcs:
+                    ref = O.csr_bfs(nv, off, col, src)[0]
+                    g.bfs_device_only(src)
+                    d, p = g.result()  # first reader: the unpack decodes the codes
+                    assert np.array_equal(d, ref), (relabel, direction, src)
+                    assert O.validate(nv, off, col, src, d, p) == 0
+                    val = g.validate()  # folds the records into st
+                    assert val["errors"] == 0 and val["reached"] == int((ref != INF).sum())
+                    d2, p2 = g.result()  # again, from the folded state
+                    assert np.array_equal(d2, d) and np.array_equal(p2, p)
+                _, _, st = g.bfs(srcs[0])
+                ref = O.csr_bfs(nv, off, col, srcs[0])[0]
+                assert st["m_comp"] == O.mcomp(u, v, ref)
+    finally:
+        ctx.set_option("relabel", "on")
+        ctx.set_option("direction", "auto")
+
+
 @pytest.mark.diag
 @pytest.mark.parametrize("abort_at", [0, 3])
 def test_persistent_abort_falls_back(ctx, abort_at):
