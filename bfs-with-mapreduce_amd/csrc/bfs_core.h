@@ -401,8 +401,6 @@ struct BlockQueueT {
     uint32_t gbase;
 };
 using BlockQueue = BlockQueueT<kQCap>;
-// the partitioned push kernels also hold a remote-pair queue: half-size queues keep 4 workgroups per CU
-using DistQueue = BlockQueueT<kQCap / 2>;
 // Single-device push kernels: winners are queued with their parent (vertex | parent << 32, same LDS bytes as
 // BlockQueue); a flush writes the next frontier's ids and, with a push log, the pairs at the same positions.
 template <int kCapT>
@@ -413,6 +411,9 @@ struct LogQueueT {
     uint32_t gbase;
 };
 using LogQueue = LogQueueT<kQCap / 2>;
+// the partitioned push kernels queue (vertex, parent) pairs too, so that their winners go to the push log like one
+// device's (round 5); they also hold a remote-pair queue
+using DistQueue = LogQueueT<kQCap / 2>;
 
 // All 64 lanes of every wave call this (wave-uniform control flow).
 template <class Q>

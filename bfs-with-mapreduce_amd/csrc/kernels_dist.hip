@@ -15,9 +15,10 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
                                                       LevelSlot *ring, int level, uint32_t lo, u64 slot,
                                                       uint32_t nrows, u64 *err, int64_t *sums, u64 *ctr, int nctr,
-                                                      u64 *arrive, int rank, int nranks) {
+                                                      u64 *arrive, int rank, int nranks, u64 *__restrict__ plog) {
     LevelSlot *cn = ring + (level + 1) % 3;
-    __shared__ BlockQueue q;
+    __shared__ LogQueue q; // plog (the push log's segment of this level): winners as (vertex, parent) pairs
+    using Q = LogQueue;
     bq_init(q);
     __syncthreads();
     const int32_t nd = level + 1;
@@ -26,7 +27,7 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     for (u64 i0 = (u64)blockIdx.x * kBS; i0 < npairs; i0 += (u64)gridDim.x * kBS) {
         const u64 i = i0 + threadIdx.x;
         bool win = false;
-        uint32_t vl = 0;
+        uint32_t vl = 0, parent = 0;
         bool have = i < npairs;
         u64 at = i;
         if (have && slot) { // the own slot is not exchanged (plan_slots): skipped
@@ -40,17 +41,18 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
             vl = (uint32_t)(pr >> 32) - lo;
             if (id_ok(vl, nrows, err) && claim(vl, vis, attempts)) {
                 win = true;
-                stt[vl] = pack_state((uint32_t)pr, nd);
+                parent = (uint32_t)pr;
+                if (!plog) stt[vl] = pack_state(parent, nd);
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
                 acc_mf += dg;
                 acc_dmax = dg > acc_dmax ? dg : acc_dmax;
             }
         }
-        bq_push(q, win, vl);
+        q_push(q, win, vl, parent);
         __syncthreads();
-        if (q.n > (uint32_t)(kQCap - kBS)) bq_flush(q, qout, &cn->qtail);
+        if (q.n > Q::kCap - (uint32_t)kBS) q_flush(q, qout, plog, &cn->qtail);
     }
-    bq_flush(q, qout, &cn->qtail);
+    q_flush(q, qout, plog, &cn->qtail);
     shard_add(cn, 0, acc_mf, 0, attempts, 0, acc_dmax);
     if (!sums) return;
     // the level close in the last workgroup to arrive (no k_level_sums dispatch): every wave's queue and
@@ -212,6 +214,9 @@ int dist_ws(bfsx_graph *g) {
     int rc = ws_alloc(g);
     if (rc) return rc;
     if (!g->ws->d_dist_ctr) BFSX_HIP_TRY(hipMalloc(&g->ws->d_dist_ctr, kCtrWords * sizeof(u64)));
+    // the push log (nv entries: a vertex is discovered once), before the first collective of the first BFS
+    if (g->ctx->opt.push_log && !g->ws->plog)
+        BFSX_HIP_TRY(hipMalloc(&g->ws->plog, (size_t)std::max<int64_t>(g->nv, 1) * sizeof(u64)));
     if (!g->ws->h_post) {
         BFSX_HIP_TRY(hipHostMalloc(&g->ws->h_post, kPostWords * sizeof(u64),
                                    hipHostMallocMapped | hipHostMallocCoherent));
@@ -360,11 +365,11 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     if (ws->off32)
         hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, ws->off32, ws->vis,
                            ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
-                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks);
+                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks, nullptr);
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
                            ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
-                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks);
+                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks, nullptr);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
@@ -715,6 +720,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         BFSX_HIP_TRY(hipEventRecord(ws->ev_begin[level], st));
         const bool td = dir == BFSX_DIR_TOPDOWN;
         bool summed = false; // the level's last kernel already closed the level (k_claim_remote)
+        u64 *plog = nullptr; // a push level's push-log segment
         const bool was_snapped = snapped;
         snapped = false;
         int64_t nq = ws->d_nf; // the push queue's length
@@ -780,7 +786,11 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                                     {"state", ws->st}, {"remote", pt.remote}, {"slot_out", pt.slot_out},
                                     {"counters", ws->d_dist_ctr}, {"front", ws->front}}))
                 return e;
-            if (int e = launch_td<true>(g, ws, nq, ws->d_mf, dmax_local, level, pt)) return e;
+            // the push log (option push_log, as on one device): this level's winners, local claims and remote ones
+            // alike, are (vertex, parent) pairs at their queue positions in the log segment [log_n, log_n + n_f)
+            plog = opt.push_log ? ws->plog + ws->log_n : nullptr;
+            if (int e = launch_td<true>(g, ws, nq, ws->d_mf, dmax_local, level, pt, false, nullptr, 0, nullptr, plog))
+                return e;
             if (!slot) {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
                                    (uint32_t)g->chunk, P, dcount);
@@ -810,12 +820,12 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                     hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
                                        (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive,
-                                       g->rank, g->nranks);
+                                       g->rank, g->nranks, plog);
                 else
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
                                        (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive,
-                                       g->rank, g->nranks);
+                                       g->rank, g->nranks, plog);
                 BFSX_LAUNCHED(st);
                 summed = true;
             }
@@ -920,6 +930,11 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         examined += h[3];
         visited_local += h[0];
         if (td) std::swap(ws->qa, ws->qb);
+        if (plog && h[0] > 0) { // the level's local winners are log entries [log_n, log_n + n_f)
+            ws->log_n += h[0];
+            ws->log_end.push_back(ws->log_n);
+            ws->log_nd.push_back(level + 1);
+        }
         dmax_local = td ? h[7] : (h[7] == 0 ? (int64_t)opt.hub_degree : -1);
         nf_core = td ? -1 : h[1]; // a pull level's local discoveries below leaf_lo (k_bu counts them in m_f)
         rank_nf.assign(h + 11, h + 11 + P);
@@ -944,6 +959,10 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
     }
     cm->tag = -2;
     recs.finish();
+    if (ws->log_n > 0) { // scattered into st by bfs_resolve / the unpack, outside the timed region
+        ws->logs_pending = true;
+        ws->resolved = false;
+    }
     if ((rc = dist_finish(g))) return rc;
     if (stats) {
         *stats = bfsx_stats{};
