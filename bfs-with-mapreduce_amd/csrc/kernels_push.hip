@@ -18,8 +18,10 @@ constexpr uint32_t kVisPref = 1u << 16; // ids whose visited bits the hub bin sn
 // s_vp / vpref (the hub bin of a relabelled single-device graph, option hub_lds_skip): the visited bits of ids below
 // vpref as they stood when the level began, in LDS.  A target whose bit is set there needs no global probe -- on the
 // hub-core level most edges of a degree-ordered hub row start with other hubs, visited a level earlier.
-template <bool kDist, class OffT, class ScanT, class Q>
-__device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg, const uint32_t *s_u, int n,
+__device__ __forceinline__ uint32_t vl_of(uint32_t v, const Part &pt) { return v - pt.lo; }
+
+template <bool kDist, class OffT, class ScanT, class BegT, class Q>
+__device__ inline void sweep_segments(const ScanT *s_scan, const BegT *s_beg, const uint32_t *s_u, int n,
                                       uint64_t x_begin, uint64_t x_end, const OffT *__restrict__ row_off,
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
                                       uint32_t *__restrict__ par, uint8_t *__restrict__ pcode, int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
@@ -42,7 +44,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
                     if ((uint64_t)s_scan[mid] <= x) lo = mid;
                     else hi = mid - 1;
                 }
-                v[k] = col[s_beg[lo] + (int64_t)(x - (uint64_t)s_scan[lo])];
+                v[k] = col[(int64_t)s_beg[lo] + (int64_t)(x - (uint64_t)s_scan[lo])];
                 pu[k] = s_u[lo] + pt.lo; // global id of the frontier vertex
             }
         }
@@ -51,7 +53,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const int64_t *s_beg,
             bool win = false, send = false;
             uint32_t vl = v[k];
             if (kDist) {
-                send = valid[k] && (v[k] / pt.chunk) != pt.rank;
+                send = valid[k] && vl_of(v[k], pt) >= pt.chunk; // outside this rank's id range [lo, lo + chunk)
                 vl = v[k] - pt.lo;
             }
             const bool known = vpref && vl < vpref && ((s_vp[vl >> 6] >> (vl & 63u)) & 1ull);
@@ -173,8 +175,12 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     } else {
         vpref = 0u;
     }
-    __shared__ u64 s_scan[kHubBatch + 1];
-    __shared__ int64_t s_beg[kHubBatch];
+    // 32-bit row offsets (nnz < 2^32) make every edge prefix and row start of a batch fit 32 bits: half the LDS
+    // of 64-bit ones, which keeps 4 workgroups per CU beside the queues (and the hub_lds_skip snapshot)
+    using ScanT = typename std::conditional<sizeof(OffT) == 4, uint32_t, u64>::type;
+    using BegT = typename std::conditional<sizeof(OffT) == 4, uint32_t, int64_t>::type;
+    __shared__ ScanT s_scan[kHubBatch + 1];
+    __shared__ BegT s_beg[kHubBatch];
     __shared__ uint32_t s_u[kHubBatch];
     __shared__ u64 s_tsum[kBS];
     __shared__ typename std::conditional<kDist, DistQueue, LogQueue>::type q;
@@ -201,7 +207,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
                 const bool ok = id_ok(u, pt.nrows, pt.err);
                 const int64_t b = ok ? (int64_t)row_off[u] : 0;
                 d[k] = ok ? (u64)((int64_t)row_off[u + 1] - b) : 0ull;
-                s_beg[idx] = b;
+                s_beg[idx] = (BegT)b;
                 s_u[idx] = ok ? u : 0u;
             }
             local += d[k];
@@ -220,10 +226,10 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int idx = (int)tid * kPer + k;
-            s_scan[idx] = (idx < hb) ? run : total;
+            s_scan[idx] = (ScanT)((idx < hb) ? run : total);
             run += d[k];
         }
-        if (tid == 0) s_scan[kHubBatch] = total;
+        if (tid == 0) s_scan[kHubBatch] = (ScanT)total;
         __syncthreads();
         // this workgroup's equal share of the batch's edges
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
