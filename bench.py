@@ -48,23 +48,35 @@ def load_module(name, file):
     return mod
 
 
-def level_bytes(ls, nwords, off_bytes=4, found_bytes=4):
+def found_store_bytes(ls, found_bytes=4, code_bytes=1):
+    """Stores of a pull or hybrid level's discoveries.  Round 5 (single device): every discovery stores a 1-B
+    provenance code (code_bytes), and the `explicit_parents` among them also a found_bytes parent; the others'
+    parent is one of their first four row entries, which the level read anyway.  A partitioned loop stores every
+    parent explicitly and no code (code_bytes 0).  Records without the counter (older builds): found_bytes each."""
+    f = ls["frontier_out"]
+    if "explicit_parents" not in ls:
+        return found_bytes * f
+    return code_bytes * f + found_bytes * ls["explicit_parents"]
+
+
+def level_bytes(ls, nwords, off_bytes=4, found_bytes=4, code_bytes=1):
     """Algorithmic bytes of one level: what the level must move at minimum, counted from
     its device counters.  Frontier-bit and visited-bit probes are not counted (the n/8-byte bitmaps are
     cache-resident).  off_bytes: width of the row offsets the traversal kernels read (uint32 when the
-    graph has < 2^32 adjacency entries).  found_bytes: the store of a pull or hybrid level's discovery (4: the
-    4-B parent, whose distance is the level's record bitmap; 8: a packed (parent, dist) state word)."""
+    graph has < 2^32 adjacency entries).  found_bytes / code_bytes: the stores of a pull or hybrid level's
+    discoveries (found_store_bytes; 4: the 4-B parent, whose distance is the level's record bitmap; 8: a packed
+    (parent, dist) state word)."""
     d = ls["direction"]
     if d in (2, 4):  # bottom-up (4: the sparse pull kernel of the tail levels, same accounting): visited word read + next word write, top1 of every live candidate, rest[]
         # (2nd..4th neighbours + degree, 16 B) of every top1 miss, the offset pair of each row walked past
         # its first four entries (`claims`), the adjacency entries walked there, the parent (or packed state)
         # of every vertex found
         return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 16 * ls["stage2"] + 2 * off_bytes * ls["claims"]
-                + 4 * ls["walked"] + found_bytes * ls["frontier_out"])
+                + 4 * ls["walked"] + found_store_bytes(ls, found_bytes, code_bytes))
     if d == 3:  # hybrid: the pull half's bitmap pass + top1 of the live candidates, the push half's rows, the
         # parent of every vertex found (both halves store the 4-B parent; the distance is the level's record)
         return (16 * nwords + 4 * max(ls["unvisited_in"], 0) + 4 * max(ls["scanned"], 0)
-                + found_bytes * ls["frontier_out"])
+                + found_store_bytes(ls, found_bytes, code_bytes))
     # top-down: queue read + offset pair per frontier vertex, adjacency rows, winners' packed state write,
     # queue append and offset pair (degree) lookup
     return ((4 + 2 * off_bytes) * ls["frontier_in"] + 4 * max(ls["mf_in"], 0)
@@ -223,15 +235,15 @@ class LevelAccount:
     """Algorithmic bytes of the timed BFS runs: per bottom-up launch (the dominant kernel) and summed
     over every level of every BFS (the whole-BFS figure)."""
 
-    def __init__(self, nwords, off_bytes, found_bytes=4):
-        self.nwords, self.off_bytes, self.found_bytes = nwords, off_bytes, found_bytes
+    def __init__(self, nwords, off_bytes, found_bytes=4, code_bytes=1):
+        self.nwords, self.off_bytes, self.found_bytes, self.code_bytes = nwords, off_bytes, found_bytes, code_bytes
         self.bu_bytes, self.bu_ms, self.bu_launches = 0, 0.0, 0
         self.all_bytes = 0
         self.by_dir = {1: 0, 2: 0, 3: 0}
 
     def add(self, levels):
         for ls in levels:
-            b = level_bytes(ls, self.nwords, self.off_bytes, self.found_bytes)
+            b = level_bytes(ls, self.nwords, self.off_bytes, self.found_bytes, self.code_bytes)
             self.all_bytes += b
             self.by_dir[ls["direction"]] = self.by_dir.get(ls["direction"], 0) + b
             if ls["direction"] == 2:
@@ -554,7 +566,7 @@ def run_dist(args, world, rank, local_rank):
             g.dist_bfs(r, want_stats=False)
 
     off_bytes = 4 if g.nnz < 0xFFFFFFFF and "offset_bits=64" not in args.option else 8
-    acct = LevelAccount(part["chunk"] // 64, off_bytes)
+    acct = LevelAccount(part["chunk"] // 64, off_bytes, code_bytes=0)  # a partition's pull parents are explicit
     # The K steps run back to back between two barrier + device-synchronise brackets (the contract's
     # timed region); every BFS is collective, so the ranks stay in step through its RCCL calls.
     ctx.synchronize()

@@ -68,7 +68,7 @@ class LevelStat(C.Structure):
         ("direction", C.c_int32), ("level", C.c_int32), ("frontier_in", C.c_int64),
         ("frontier_out", C.c_int64), ("mf_in", C.c_int64), ("unvisited_in", C.c_int64),
         ("scanned", C.c_int64), ("claims", C.c_int64), ("kernel_ms", C.c_double), ("cum_ms", C.c_double),
-        ("stage2", C.c_int64), ("walked", C.c_int64),
+        ("stage2", C.c_int64), ("walked", C.c_int64), ("explicit_parents", C.c_int64),
     ]
 
 

@@ -64,9 +64,10 @@ struct alignas(64) StatShard {
     u64 stage2;  // bottom-up: candidates that loaded rest[] (stage A2, 16 B each)
     u64 walked;  // bottom-up: adjacency entries read from col in phase B (4 B each)
     u64 nhub;    // bottom-up, single device: vertices found below hub_row_lim (the only possible hubs)
+    u64 expl;    // discoveries that stored an explicit 4-B parent (provenance code kCodeExplicit; bytes accounting)
     u64 dmax;    // top-down: largest degree in the produced frontier (skips the hub bin when <= hub_deg)
 };
-constexpr int kStatFields = 8; // summed fields, in declaration order (dmax is a max)
+constexpr int kStatFields = 9; // summed fields, in declaration order (dmax is a max)
 
 // Counters of one level.  Level L reads slot L%3 (its own frontier, already on the host), accumulates
 // the frontier it produces into slot (L+1)%3 and zeroes slot (L+2)%3: no per-level memset.
@@ -108,7 +109,7 @@ struct alignas(64) PersistOut {
 // A level's counter sums as the host reads them (mapped pinned memory, written by publish_if_last).
 struct alignas(64) Published {
     u64 seq;
-    int64_t qtail, nf, mf, sc, cl, mu, dmax, stage2, walked, nhub;
+    int64_t qtail, nf, mf, sc, cl, mu, dmax, stage2, walked, nhub, expl;
 };
 
 struct BfsWorkspace {
@@ -302,12 +303,12 @@ __device__ inline uint32_t wave_max32(uint32_t x) { // one lane exchange per ste
 }
 
 __device__ inline void shard_add(LevelSlot *slot, u64 nf, u64 mf, u64 scanned, u64 claims, u64 mu, u64 dmax = 0,
-                                 u64 stage2 = 0, u64 walked = 0, u64 nhub = 0) {
+                                 u64 stage2 = 0, u64 walked = 0, u64 nhub = 0, u64 expl = 0) {
     __shared__ u64 s_red[kStatFields][kWaves];
     __shared__ u64 s_dmax[kWaves];
     dmax = wave_max(dmax);
     if (lane_id() == 0) s_dmax[threadIdx.x >> 6] = dmax;
-    u64 v[kStatFields] = {nf, mf, scanned, claims, mu, stage2, walked, nhub};
+    u64 v[kStatFields] = {nf, mf, scanned, claims, mu, stage2, walked, nhub, expl};
     const unsigned wave = threadIdx.x >> 6;
 #pragma unroll
     for (int f = 0; f < kStatFields; f++) {
@@ -366,7 +367,10 @@ __device__ inline void publish_if_last(LevelSlot *slot, Published *pub, u64 seq)
         auto ld = [](const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
         const u64 nf = wave_sum(ld(sh + 0)), mf = wave_sum(ld(sh + 1)), sc = wave_sum(ld(sh + 2)),
                   cl = wave_sum(ld(sh + 3)), mu = wave_sum(ld(sh + 4)), s2 = wave_sum(ld(sh + 5)),
-                  wk = wave_sum(ld(sh + 6)), nh = wave_sum(ld(sh + 7)), dmax = wave_max(ld(sh + 8));
+                  wk = wave_sum(ld(sh + 6)), nh = wave_sum(ld(sh + 7)), ex = wave_sum(ld(sh + 8)),
+                  dmax = wave_max(ld(sh + 9));
+        static_assert(offsetof(StatShard, expl) == 8 * sizeof(u64) && offsetof(StatShard, dmax) == 9 * sizeof(u64),
+                      "publish_if_last reads the shard fields by position");
         const u64 qt = ld(&slot->qtail);
         if (lane == 0) {
             // mapped host memory (uncached): the record's stores complete before the sequence number's
@@ -374,6 +378,7 @@ __device__ inline void publish_if_last(LevelSlot *slot, Published *pub, u64 seq)
             vp->stage2 = (int64_t)s2;
             vp->walked = (int64_t)wk;
             vp->nhub = (int64_t)nh;
+            vp->expl = (int64_t)ex;
             vp->qtail = (int64_t)qt;
             vp->nf = (int64_t)nf;
             vp->mf = (int64_t)mf;
@@ -681,7 +686,7 @@ constexpr uint32_t kHubBit = 0x40000000u; // hub encoding needs every global id 
 constexpr uint32_t kHubMask = kHubBit - 1u;
 
 struct SlotSums {
-    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0, nh = 0;
+    int64_t nf = 0, mf = 0, sc = 0, cl = 0, mu = 0, s2 = 0, wk = 0, nh = 0, ex = 0;
 };
 
 // ---- host entry points of the kernel families (definitions in the .hip file named) ----------------

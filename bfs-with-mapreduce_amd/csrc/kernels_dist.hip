@@ -424,6 +424,7 @@ int dist_level_end(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local) {
     ls.claims = s.cl;
     ls.stage2 = s.s2;
     ls.walked = s.wk;
+    ls.explicit_parents = s.ex;
     g->level_stats.push_back(ls);
     g->level_dirs.push_back(ws->d_dir);
     if (td) std::swap(ws->qa, ws->qb);
@@ -925,6 +926,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         ls.claims = h[4];
         ls.stage2 = h[5];
         ls.walked = h[6];
+        ls.explicit_parents = td ? 0 : h[0]; // a partition's pull levels store every parent explicitly
         g->level_stats.push_back(ls);
         g->level_dirs.push_back(dir);
         examined += h[3];

@@ -562,6 +562,7 @@ SlotSums sum_slot(const LevelSlot *s) {
         r.mu += (int64_t)s->sh[i].mu;
         r.s2 += (int64_t)s->sh[i].stage2;
         r.wk += (int64_t)s->sh[i].walked;
+        r.ex += (int64_t)s->sh[i].expl;
         r.nh += (int64_t)s->sh[i].nhub;
     }
     return r;
@@ -774,6 +775,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             ls.unvisited_in = nv - visited - n_pre;
             ls.scanned = ws->h_pub->sc;
             ls.claims = ws->h_pub->cl;
+            ls.explicit_parents = ws->h_pub->expl;
             g->level_stats.push_back(ls);
             timing.push_back({level, false, 0.0, 0.0});
             examined += ls.scanned;
@@ -923,6 +925,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         s.mu = ws->h_pub->mu;
         s.s2 = ws->h_pub->stage2;
         s.wk = ws->h_pub->walked;
+        s.ex = ws->h_pub->expl;
         const int64_t nf_new = (dir == BFSX_DIR_TOPDOWN) ? ws->h_pub->qtail : s.nf;
         if (plog && nf_new > 0) { // the level's winners are log entries [log_n, log_n + nf_new)
             ws->log_n += nf_new;
@@ -943,6 +946,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         ls.claims = s.cl;
         ls.stage2 = s.s2;
         ls.walked = s.wk;
+        ls.explicit_parents = s.ex;
         g->level_stats.push_back(ls);
         timing.push_back({level, false, 0.0, 0.0});
         examined += ls.scanned;

@@ -163,6 +163,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
     const int32_t nd = level + 1;
     // per-lane counters fit 32 bits (a lane sees a few hundred candidates per launch); widened at the end
     uint32_t acc_nf = 0, acc_mf = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0, acc_nh = 0;
+    uint32_t acc_ex = 0; // discoveries with an explicit 4-B parent
     const int64_t wstride = (int64_t)gridDim.x * kWaves * 64;
     for (int64_t w0 = ((int64_t)blockIdx.x * kWaves + wave) * 64; w0 < nwords; w0 += wstride) {
         const int64_t wl = w0 + lane;
@@ -295,6 +296,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         settle_state(stt, par_out, code_out, v[k], code, probe_id<kHubs>(hub_id, par), nd);
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
+                        acc_ex += code == kCodeExplicit ? 1u : 0u;
                         if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
                         else if (!kHubOnly) { // single device: non-leaves found, and possible hubs found
                             acc_mf += v[k] < leaf_lo ? 1u : 0u;
@@ -355,6 +357,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                             settle_state(stt, par_out, code_out, vv, kCodeExplicit, probe_id<kHubs>(hub_id, par), nd);
                             atomicOr(&s_nx[wave][(vv - vbase) >> 6], 1ull << (vv & 63u));
                             acc_nf += 1;
+                            acc_ex += 1;
                             if (kMf) acc_mf += (uint32_t)(e - b);
                             else if (!kHubOnly) {
                                 acc_mf += vv < leaf_lo ? 1u : 0u;
@@ -379,7 +382,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
         }
     }
     // claims field: rows walked (phase B)
-    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk, acc_nh);
+    shard_add(cn, acc_nf, acc_mf, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk, acc_nh, acc_ex);
     publish_if_last(cn, pub, seq);
 }
 
@@ -444,6 +447,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
     const int32_t nd = level + 1;
     constexpr int kC = kSparseWords / 64;
     uint32_t acc_nf = 0, acc_q = 0, acc_sc = 0, acc_mu = 0, acc_rows = 0, acc_s2 = 0, acc_wk = 0, acc_nh = 0;
+    uint32_t acc_ex = 0; // discoveries with an explicit 4-B parent
     const uint32_t *front32 = reinterpret_cast<const uint32_t *>(front);
     auto fbit = [&](uint32_t x) -> uint32_t { return (front32[x >> 5] >> (x & 31u)) & 1u; };
     int64_t wb = 0; // first word of the wave's current range
@@ -453,6 +457,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
             settle_state(stt, par_out, code_out, v, code, par, nd);
             atomicOr(&s_nx[wave][(int64_t)(v >> 6) - wb], 1ull << (v & 63u));
             acc_nf += 1;
+            acc_ex += code == kCodeExplicit ? 1u : 0u;
             acc_nh += v < hub_row_lim ? 1u : 0u;
         }
         const bool q = found && v < qlim;
@@ -622,7 +627,7 @@ __global__ __launch_bounds__(kBS) void k_bu_sparse(const OffT *__restrict__ row_
         __builtin_amdgcn_wave_barrier();
     }
     // claims field: rows walked (phase B); mf field: discoveries queued
-    shard_add(cn, acc_nf, acc_q, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk, acc_nh);
+    shard_add(cn, acc_nf, acc_q, acc_sc, acc_rows, acc_mu, 0, acc_s2, acc_wk, acc_nh, acc_ex);
     publish_if_last(cn, pub, seq);
 }
 

@@ -26,7 +26,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const BegT *s_beg, co
                                       const uint32_t *__restrict__ col, u64 *vis, u64 *__restrict__ stt,
                                       uint32_t *__restrict__ par, uint8_t *__restrict__ pcode, int32_t nd, Q &q, uint32_t *__restrict__ qout, u64 *qtail,
                                       const Part &pt, RemoteQueue *rq, u64 &acc_mf, u64 &attempts, u64 &acc_dmax,
-                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh, u64 *__restrict__ plog,
+                                      HubSet hs, u64 &acc_mfh, u64 &acc_nh, u64 &acc_ex, u64 *__restrict__ plog,
                                       const u64 *s_vp = nullptr, uint32_t vpref = 0u) {
     for (uint64_t x0 = x_begin; x0 < x_end; x0 += (uint64_t)kBS * kItems) {
         uint32_t v[kItems], pu[kItems];
@@ -64,6 +64,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const BegT *s_beg, co
                 if (par) {
                     par[vl] = pu[k];
                     if (pcode) pcode[vl] = kCodeExplicit;
+                    acc_ex++;
                 }
                 else if (!plog) stt[vl] = pack_state(pu[k], nd);
                 const u64 dg = (u64)(row_off[vl + 1] - row_off[vl]);
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     if (kDist && threadIdx.x == 0) rq->n = 0;
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0, acc_ex = 0;
     // gsz (<= kBS) frontier vertices per workgroup and step: a narrow frontier spreads over more
     // workgroups, so each sweeps its rows in one step instead of several dependent ones
     for (uint32_t base = blockIdx.x * gsz; base < qlen; base += gridDim.x * gsz) {
@@ -147,13 +148,13 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
         }
         __syncthreads();
         sweep_segments<kDist>(s_scan, s_beg, s_u, gsz, 0, total, row_off, col, vis, stt, par, pcode, nd, q, qout, &cn->qtail, pt,
-                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog);
+                              rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, acc_ex, plog);
         __syncthreads();
     }
     q_flush(q, qout, plog, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
     // top-down: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
-    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh, acc_ex);
     publish_if_last(cn, pub, seq);
     if (kDist) slot_headers_if_last(pt);
 }
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x;
     constexpr int kPer = kHubBatch / kBS;
-    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0;
+    u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0, acc_ex = 0;
     __syncthreads();
     for (uint32_t h0 = 0; h0 < nh; h0 += kHubBatch) {
         const int hb = (int)min((uint32_t)kHubBatch, nh - h0);
@@ -235,12 +236,12 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
         const uint64_t x_begin = total * blockIdx.x / gridDim.x, x_end = total * (blockIdx.x + 1) / gridDim.x;
         if (tid == 0) scanned += x_end - x_begin;
         sweep_segments<kDist>(s_scan, s_beg, s_u, hb, x_begin, x_end, row_off, col, vis, stt, par, pcode, nd, q, qout,
-                              &cn->qtail, pt, rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, plog, s_vp, vpref);
+                              &cn->qtail, pt, rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, acc_ex, plog, s_vp, vpref);
         __syncthreads();
     }
     q_flush(q, qout, plog, &cn->qtail);
     if (kDist) rq_flush(*rq, pt);
-    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh);
+    shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh, acc_ex);
     publish_if_last(cn, pub, seq);
     if (kDist) slot_headers_if_last(pt);
 }

@@ -84,6 +84,8 @@ typedef struct bfsx_level_stat {
     int64_t stage2;        /* bottom-up: candidates that read their 2nd..4th neighbours (16-B rest[] load) */
     int64_t walked;        /* bottom-up: adjacency entries read from the CSR past the first four (phase B);
                             * top-down on a partitioned graph: (vertex, parent) pairs this rank sent to others */
+    int64_t explicit_parents; /* pull and hybrid levels: discoveries that stored a 4-B parent (the others a 1-B
+                               * provenance code only: their parent is their first, 2nd, 3rd or 4th row entry) */
 } bfsx_level_stat;
 
 /* ---- library / context ---------------------------------------------------------------------- */

@@ -26,6 +26,22 @@ def test_bottom_up_level_bytes(bench):
     assert bench.level_bytes(ls, nwords, found_bytes=8) == 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50 + 8 * 600
 
 
+def test_pull_level_bytes_with_provenance_codes(bench):
+    """Round 5: a single-device pull level stores a 1-B code per discovery plus a 4-B parent for its
+    explicit_parents; a partition's pull level stores every parent explicitly and no code (code_bytes 0)."""
+    ls = {"direction": 2, "unvisited_in": 1000, "stage2": 100, "claims": 10, "walked": 50, "frontier_out": 600,
+          "explicit_parents": 40}
+    base = 16 * 64 + 4 * 1000 + 16 * 100 + 8 * 10 + 4 * 50
+    assert bench.level_bytes(ls, 64) == base + 1 * 600 + 4 * 40
+    dist = dict(ls, explicit_parents=600)
+    assert bench.level_bytes(dist, 64, code_bytes=0) == base + 4 * 600
+    hy = {"direction": 3, "unvisited_in": 1000, "scanned": 300, "frontier_out": 20, "explicit_parents": 5}
+    assert bench.level_bytes(hy, 64) == 16 * 64 + 4 * 1000 + 4 * 300 + 20 + 4 * 5
+    acct = bench.LevelAccount(64, 4, code_bytes=0)
+    acct.add([dict(dist, kernel_ms=0.1)])
+    assert acct.bu_bytes == base + 4 * 600
+
+
 def test_top_down_level_bytes(bench):
     ls = {"direction": 1, "frontier_in": 10, "mf_in": 300, "frontier_out": 20}
     # uint32 row offsets (the default below 2^32 adjacency entries), then int64 offsets

@@ -334,6 +334,15 @@ def test_provenance_codes_every_reader(ctx, relabel, direction):
                 _, _, st = g.bfs(srcs[0])
                 ref = O.csr_bfs(nv, off, col, srcs[0])[0]
                 assert st["m_comp"] == O.mcomp(u, v, ref)
+                # the bytes accounting's counter: explicit parents only where a discovery needed one
+                ls = g.level_stats()
+                assert all(0 <= l["explicit_parents"] <= l["frontier_out"] for l in ls)
+                assert all(l["explicit_parents"] == 0 for l in ls if l["direction"] == 1)
+                pulled = [l for l in ls if l["direction"] in (2, 4)]
+                if nv == side * side and direction == "bottomup":  # rows of <= 4 entries: codes only
+                    assert pulled and sum(l["explicit_parents"] for l in pulled) == 0
+                if nv == 1 << 14 and direction == "bottomup":  # Kronecker rows walked past their 4th entry
+                    assert sum(l["explicit_parents"] for l in pulled) > 0
     finally:
         ctx.set_option("relabel", "on")
         ctx.set_option("direction", "auto")
