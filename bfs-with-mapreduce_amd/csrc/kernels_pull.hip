@@ -296,7 +296,7 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
                         settle_state(stt, par_out, code_out, v[k], code, probe_id<kHubs>(hub_id, par), nd);
                         atomicOr(&s_nx[wave][(v[k] - vbase) >> 6], 1ull << (v[k] & 63u));
                         acc_nf += 1;
-                        acc_ex += code == kCodeExplicit ? 1u : 0u;
+                        if (kHubs) acc_ex += 1; // phase A names its parent by code 0-3, except the hub domain
                         if (kMf) acc_mf += deg ? deg : (uint32_t)(row_off[v[k] + 1] - row_off[v[k]]);
                         else if (!kHubOnly) { // single device: non-leaves found, and possible hubs found
                             acc_mf += v[k] < leaf_lo ? 1u : 0u;
