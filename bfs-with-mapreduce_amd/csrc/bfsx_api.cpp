@@ -482,9 +482,13 @@ static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
         return BFSX_OK;
     }
     if (k == "slot_pairs") {
+        if (v == "auto") {
+            ctx->opt.slot_pairs = -1;
+            return BFSX_OK;
+        }
         char *end = nullptr;
         const long long x = strtoll(value, &end, 10);
-        if (!end || *end || x < 0) return fail(BFSX_E_ARG, "slot_pairs must be a pair count >= 0");
+        if (!end || *end || x < 0) return fail(BFSX_E_ARG, "slot_pairs must be auto or a pair count >= 0");
         ctx->opt.slot_pairs = x;
         return BFSX_OK;
     }

@@ -50,7 +50,7 @@ struct Options {
     bool bu_pipeline = true;    // bottom-up: the next round's top1 loads overlap this round (kU = 4)
     int bu_sparse = 64;          // single device: pull levels with <= n/bu_sparse unvisited candidates run k_bu_sparse (0 off)
     bool bu_lds_prefix = true;  // pull kernels: the frontier bits of the 2^16 lowest (highest-degree) ids in LDS
-    int64_t slot_pairs = 16384; // partitioned push levels with a global m_f up to this: fixed exchange slots
+    int64_t slot_pairs = -1;    // partitioned push levels with a global m_f up to this: fixed exchange slots (-1: auto)
     // partitioned: ids of degree above big_degree (at most big_cap per rank) are listed with their degree
     // on every rank (read at a graph's first partitioned BFS; see dist_big_list)
     int64_t big_degree = 4096;

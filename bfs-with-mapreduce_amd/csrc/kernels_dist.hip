@@ -23,17 +23,18 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
     __syncthreads();
     const int32_t nd = level + 1;
     u64 acc_mf = 0, attempts = 0, acc_dmax = 0;
-    // slot > 0: npairs = P * slot entries in P fixed slots of [count, slot pairs] (small levels)
+    // slot > 0: the P fixed slots of [count, slot pairs] (small levels); npairs = (P - 1) * slot, the peers' slots
     for (u64 i0 = (u64)blockIdx.x * kBS; i0 < npairs; i0 += (u64)gridDim.x * kBS) {
         const u64 i = i0 + threadIdx.x;
         bool win = false;
         uint32_t vl = 0, parent = 0;
         bool have = i < npairs;
         u64 at = i;
-        if (have && slot) { // the own slot is not exchanged (plan_slots): skipped
-            const u64 p = i / slot, k = i - p * slot;
+        if (have && slot) { // npairs = (P - 1) * slot: the peers' slots (the own one is not exchanged, plan_slots)
+            const u64 pp = i / slot, k = i - pp * slot;
+            const u64 p = pp + (pp >= (u64)rank ? 1u : 0u);
             const u64 base = p * (slot + 1);
-            have = p != (u64)rank && k < pairs[base];
+            have = k < pairs[base];
             at = base + 1 + k;
         }
         if (have) {
@@ -629,6 +630,17 @@ bool sparse_exchange(const bfsx_graph *g, int64_t nf_global, const std::vector<i
     return mode == 2 || nf_global * 128 < g->nv_global;
 }
 
+// The largest global m_f a push level exchanges through fixed slots (option slot_pairs; auto: a rank sends its
+// P - 1 peers a slot of m_f + 1 words each whether it fills them or not, so the bound keeps that under 1 MiB --
+// 16,384 pairs at P = 8 as before round 5, 131,072 at P = 2 -- and at P = 1, where nothing is sent, any level of up
+// to 2^22 edges saves the count exchange and its host wait)
+int64_t slot_pairs_for(const bfsx_graph *g) {
+    const int64_t o = g->ctx->opt.slot_pairs;
+    if (o >= 0) return o;
+    const int64_t P = g->nranks;
+    return P <= 1 ? ((int64_t)1 << 22) : std::max<int64_t>(16384, ((int64_t)1 << 20) / (8 * (P - 1)));
+}
+
 int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
     cm->tag = -1;
     if (g->ctx->opt.fail_rank == g->rank && g->ctx->opt.fail_level == -2) // test hook: before any collective
@@ -667,7 +679,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         if (it != ws->h_big.end() && (int64_t)(*it >> 32) == source) deg = (int64_t)(*it & 0xFFFFFFFFull);
         mf = deg >= 0 ? deg : ws->big_thr;
     } else {
-        mf = opt.slot_pairs + 1;
+        mf = slot_pairs_for(g) + 1;
     }
     int64_t deg_local = 0;
     BFSX_HIP_TRY(hipMemsetAsync(ws->d_dist_ctr, 0, kCtrHead * sizeof(u64), st)); // before the timed region
@@ -767,7 +779,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
             // pair count read on the device: the grid is sized by its upper bound, the local m_f
             const unsigned gbk = clamp_grid((need + kBS - 1) / kBS, 1024);
             int64_t slot = 0, ro = 0; // slot > 0: fixed-slot exchange
-            if (mf <= opt.slot_pairs) {
+            if (mf <= slot_pairs_for(g)) {
                 // small level: no rank sends more than the global m_f pairs to any peer, so every peer gets
                 // a fixed slot [count, m_f pairs] -- one exchange, no count all-to-all, no host wait.  The push
                 // kernels write the pairs into the slots themselves; the last one's last workgroup writes the
@@ -780,7 +792,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                 pt.slot_cursor = dcursor;
                 pt.slot_arrive = dcount;
                 plan_slots(P, slot, plan, g->rank); // the own slot stays empty and is not exchanged
-                ro = P * slot; // candidate entries the claim kernel reads
+                ro = (int64_t)(P - 1) * slot; // candidate entries the claim kernel reads: the peers' slots
             }
             if (int e = check_live(g, ws, level, "push kernels",
                                    {{"queue in", ws->qa}, {"queue out", ws->qb}, {"hubs", ws->hubs}, {"vis", ws->vis},

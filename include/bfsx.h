@@ -144,9 +144,10 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 level, off = never)
  *   "bu_lds_prefix" = on|off (pull kernels read the frontier bits of the 2^16 highest-degree ids of a
  *                 relabelled single-device graph from a per-workgroup LDS copy; default on)
- *   "slot_pairs" = int (partitioned graphs: a push level whose frontier has at most this many edges in
+ *   "slot_pairs" = auto|int (partitioned graphs: a push level whose frontier has at most this many edges in
  *                 total exchanges its pairs through fixed per-peer slots, skipping the count all-to-all
- *                 and its host wait; default 16384, 0 = never)
+ *                 and its host wait; 0 = never; auto (default) = max(16384, 2^20 / (8 (P - 1))) pairs, so a
+ *                 rank sends its peers at most 1 MiB of slots, and 2^22 at P = 1, where nothing is sent)
  *   "build_chunk" = int (CSR build: raw adjacency entries per sort/dedup chunk, default 2^30; bounds the
  *                 build's temporary memory, so a scale-30 Kronecker graph builds on one device)
  *   "leaf_skip" = on|off (single device: the degree-1 vertices a pull level discovers stay out of the next

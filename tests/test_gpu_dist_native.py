@@ -268,7 +268,7 @@ print("rccl-ok")
     assert r.returncode == 0 and "rccl-ok" in r.stdout, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("slot_pairs", ["0", "16384", "100000000"])
+@pytest.mark.parametrize("slot_pairs", ["0", "16384", "100000000", "auto"])
 def test_native_group_exchange_modes(bfsx, slot_pairs):
     """Push-level pair exchange in both forms: counts all-to-all then variable sends (slot_pairs=0),
     fixed per-peer slots for every level (huge threshold), and the default mix; all bit-exact."""
