@@ -1035,7 +1035,7 @@ int apply_logs(bfsx_graph *g, BfsWorkspace *ws, hipEvent_t ev) {
     BFSX_HIP_TRY(hipMemcpyAsync(ws->d_log_meta, meta.data(), meta.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
     BFSX_HIP_TRY(hipStreamSynchronize(st)); // meta is a host temporary
     if (ev) BFSX_HIP_TRY(hipEventRecord(ev, st));
-    hipLaunchKernelGGL(k_resolve_log, dim3(clamp_grid((ws->log_n + 8 * kBS - 1) / (8 * kBS), 8192)), dim3(kBS), 0, st, ws->plog,
+    hipLaunchKernelGGL(k_resolve_log, dim3(clamp_grid((ws->log_n + kBS - 1) / kBS, 8192)), dim3(kBS), 0, st, ws->plog,
                        ws->log_n, ws->d_log_meta, nseg, ws->st);
     BFSX_LAUNCHED(st);
     ws->logs_pending = false;
