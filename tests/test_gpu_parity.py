@@ -348,6 +348,32 @@ def test_provenance_codes_every_reader(ctx, relabel, direction):
         ctx.set_option("direction", "auto")
 
 
+@pytest.mark.parametrize("skip", ["on", "off"])
+@pytest.mark.parametrize("direction", ["auto", "topdown"])
+def test_hub_lds_skip_option(ctx, skip, direction):
+    """Round 5, option hub_lds_skip: the hub bin (k_td_hubs) of a relabelled graph snapshots the visited bits of
+    the 2^16 lowest ids into LDS at the level's start and probes no target the snapshot marks.  Forced push
+    levels from hub roots run the hub bin with most of a level's edges pointing at earlier-visited hubs; a
+    small hub degree puts many rows into the bin.  Distances against the oracle, trees valid, on and off."""
+    ctx.set_option("hub_lds_skip", skip)
+    ctx.set_option("direction", direction)
+    ctx.set_option("hub_degree", 16)
+    try:
+        for scale, seed in ((14, 31), (16, 8)):
+            ou, ov = O.kronecker(scale, 16, seed)
+            nv = 1 << scale
+            off, col = O.build_sets(nv, ou, ov)
+            deg = np.diff(off)
+            with ctx.kronecker(scale, 16, seed) as g:
+                roots = [int(np.argmax(deg))] + [int(r) for r in g.sample_roots(3, seed=5)]
+                for r in roots:
+                    check_against_oracle(g, nv, off, col, r, ou, ov, mr=False)
+    finally:
+        ctx.set_option("hub_lds_skip", "on")
+        ctx.set_option("direction", "auto")
+        ctx.set_option("hub_degree", 64)
+
+
 @pytest.mark.diag
 @pytest.mark.parametrize("abort_at", [0, 3])
 def test_persistent_abort_falls_back(ctx, abort_at):
