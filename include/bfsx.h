@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define BFSX_ABI_VERSION 1
+/* 2 (round 5): bfsx_level_stat gained explicit_parents at its end; bfsx_init_group, bfsx_group_size,
+ * bfsx_dist_graph_load_algs4 and bfsx_last_resolve_ms were added */
+#define BFSX_ABI_VERSION 2
 
 /* Error codes.  Mapping to the reference's exceptions:
  *   E_IO    <- IOException from FileInputStream / Files.write  (GraphFileUtil.java:43,46,68)
