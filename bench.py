@@ -533,6 +533,12 @@ def run_dist(args, world, rank, local_rank):
     import torch.distributed as dist
 
     arm_deadline(args.deadline, f"rank {rank} of {world}")
+    if os.environ.get("BFSX_RCCL_SHARED_DEVICE") == "1":
+        # rehearsal of N > 1 RCCL on a box with fewer GPUs than ranks: RCCL refuses two ranks on one device of
+        # one host, so every rank presents a host id of its own and the ranks talk over RCCL's socket transport
+        # (loopback). Never set by the driver's runs; see DESIGN §7.
+        os.environ["NCCL_HOSTID"] = f"bfsx-rehearsal-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     # Gloo and RCCL print banners on the process's C-level stdout; the contract is ONE JSON line, so
     # fd 1 points at stderr until the result is printed
     sys.stdout.flush()

@@ -203,11 +203,14 @@ class RcclComm final : public Comm {
         if (!check_seq) return BFSX_OK;
         if (!d_seq) BFSX_HIP_TRY(hipMalloc(&d_seq, (kBoardRanks + 1) * sizeof(unsigned long long)));
         const unsigned long long mine = ((unsigned long long)(uint32_t)op << 32) | (uint32_t)tag;
-        BFSX_HIP_TRY(hipMemcpyAsync(d_seq, &mine, sizeof(mine), hipMemcpyHostToDevice, st));
+        // two fills instead of a copy from pageable memory, which could block the host behind a pending collective
+        BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_seq, (int)(uint32_t)mine, 1, st));
+        BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)((uint32_t *)d_seq + 1), (int)(uint32_t)(mine >> 32), 1, st));
         BFSX_NCCL_TRY(ncclAllGather(d_seq, d_seq + 1, 1, ncclUint64, comm, st));
         std::vector<unsigned long long> all(nranks);
-        BFSX_HIP_TRY(hipMemcpyAsync(all.data(), d_seq + 1, nranks * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        if (int e = comm_sync(this, st, "the collective-sequence check")) return e;
+        if (int e = comm_fetch(this, st, all.data(), d_seq + 1, nranks * sizeof(unsigned long long),
+                               "the collective-sequence check"))
+            return e;
         for (int p = 0; p < nranks; p++)
             if (all[p] != mine) {
                 const std::string m = "collective mismatch: rank " + std::to_string(rank) + " is in " + comm_op_name(op) +
@@ -282,8 +285,7 @@ int warm_up(RcclComm *c, hipStream_t st) {
     if (int e = c->allgather(reinterpret_cast<const unsigned long long *>(d + 1), 1,
                              reinterpret_cast<unsigned long long *>(d + 2 + 2 * kBoardRanks), st))
         return e;
-    BFSX_HIP_TRY(hipMemcpyAsync(h.data(), d, h.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    if (int e = comm_sync(c, st, "the communicator warm-up")) return e;
+    if (int e = comm_fetch(c, st, h.data(), d, h.size() * sizeof(int64_t), "the communicator warm-up")) return e;
     if (h[0] != P) return fail(BFSX_E_RCCL, "communicator warm-up: all-reduce returned " + std::to_string(h[0]));
     for (int p = 0; p < P; p++)
         if (p != c->rank && h[2 + kBoardRanks + p] != p)
@@ -466,6 +468,31 @@ void apply_options(Comm *c, const bfsx_ctx *ctx) {
 }
 
 } // namespace
+
+Comm::~Comm() {
+    if (pinned) (void)hipHostFree(pinned);
+}
+
+int comm_fetch(Comm *cm, hipStream_t st, void *dst, const void *d_src, size_t bytes, const char *what) {
+    if (!cm) {
+        BFSX_HIP_TRY(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, st));
+        BFSX_HIP_TRY(hipStreamSynchronize(st));
+        return BFSX_OK;
+    }
+    if (bytes > cm->pinned_bytes) {
+        // the stream may still run a collective: the old buffer is no copy's target (every fetch drains its copy)
+        if (cm->pinned) (void)hipHostFree(cm->pinned);
+        cm->pinned = nullptr;
+        cm->pinned_bytes = 0;
+        const size_t cap = std::max<size_t>(bytes, 4096);
+        BFSX_HIP_TRY(hipHostMalloc(&cm->pinned, cap, hipHostMallocDefault));
+        cm->pinned_bytes = cap;
+    }
+    BFSX_HIP_TRY(hipMemcpyAsync(cm->pinned, d_src, bytes, hipMemcpyDeviceToHost, st));
+    if (int e = comm_sync(cm, st, what)) return e;
+    std::memcpy(dst, cm->pinned, bytes);
+    return BFSX_OK;
+}
 
 int comm_sync(Comm *cm, hipStream_t st, const char *what) {
     if (!cm) {

@@ -89,7 +89,9 @@ struct Comm {
     int64_t timeout_ms = 120000; // option comm_timeout_ms: a host wait on the peers fails after this long
     bool check_seq = false;      // option check_collectives: every collective compares (op, level) across the ranks
     bool agreed = false;         // the error being returned was reached by every rank at the same point: no abort
-    virtual ~Comm() = default;
+    void *pinned = nullptr;      // comm_fetch's bounce buffer (page-locked host memory)
+    size_t pinned_bytes = 0;
+    virtual ~Comm();
     virtual int allreduce_sum(int64_t *d_buf, int n, hipStream_t st) = 0;              // in place
     // one value per rank; d_recv[rank] (the value a rank sends itself) may be left unwritten
     virtual int alltoall1(const int64_t *d_send, int64_t *d_recv, hipStream_t st) = 0;
@@ -107,6 +109,10 @@ struct Comm {
 int64_t now_ns();
 // hipStreamSynchronize for the partitioned path: polls the communicator while the stream drains
 int comm_sync(Comm *cm, hipStream_t st, const char *what);
+// Device -> host copy of a collective's result: through cm's page-locked bounce buffer, then comm_sync.  A copy
+// straight into pageable memory blocks the host until the stream reaches it, outside comm_sync's polling: a rank
+// whose peer failed would wait there for a collective that never completes.
+int comm_fetch(Comm *cm, hipStream_t st, void *dst, const void *d_src, size_t bytes, const char *what);
 // After a collective entry point returned rc on this rank: abort the group when rc is this rank's own error
 // (not a peer's abort it merely observed), so no peer waits for it.  Returns rc.
 int comm_guard(Comm *cm, int rc);

@@ -573,8 +573,7 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
     }
     if (int e = cm->allgather(b.cnt, 1, b.cnt + 1, st)) return e;
     std::vector<u64> counts(P, 0);
-    BFSX_HIP_TRY(hipMemcpyAsync(counts.data(), b.cnt + 1, P * sizeof(u64), hipMemcpyDeviceToHost, st));
-    if (int e = comm_sync(cm, st, "the degree-list all-gather")) return e;
+    if (int e = comm_fetch(cm, st, counts.data(), b.cnt + 1, P * sizeof(u64), "the degree-list all-gather")) return e;
     u64 maxc = 0;
     bool over = false;
     for (int p = 0; p < P; p++) {
@@ -594,8 +593,7 @@ int dist_big_list(bfsx_graph *g, BfsWorkspace *ws, Comm *cm) {
         BFSX_HIP_TRY(hipMemsetAsync(b.sel + mine, 0xFF, (maxc - mine) * sizeof(u64), st));
         if (int e = cm->allgather(b.sel, (int64_t)maxc, b.all, st)) return e;
         std::vector<u64> h(P * maxc);
-        BFSX_HIP_TRY(hipMemcpyAsync(h.data(), b.all, h.size() * sizeof(u64), hipMemcpyDeviceToHost, st));
-        if (int e = comm_sync(cm, st, "the degree-list all-gather")) return e;
+        if (int e = comm_fetch(cm, st, h.data(), b.all, h.size() * sizeof(u64), "the degree-list all-gather")) return e;
         for (u64 x : h)
             if (x != ~0ull) ws->h_big.push_back(x);
         std::sort(ws->h_big.begin(), ws->h_big.end());
@@ -660,8 +658,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         h[0] = g->nnz;
         BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, sizeof(int64_t), hipMemcpyHostToDevice, st));
         if (int e = cm->allreduce_sum(sums + 8, 1, st)) return e;
-        BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        if (int e = comm_sync(cm, st, "the adjacency-count all-reduce")) return e;
+        if (int e = comm_fetch(cm, st, h, sums + 8, sizeof(int64_t), "the adjacency-count all-reduce")) return e;
         ws->nnz_global = h[0];
     }
     if (ws->big_thr < 0) {
@@ -993,8 +990,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         h[1] = r;
         BFSX_HIP_TRY(hipMemcpyAsync(sums + 8, h, 2 * sizeof(int64_t), hipMemcpyHostToDevice, st));
         if (int e = cm->allreduce_sum(sums + 8, 2, st)) return e;
-        BFSX_HIP_TRY(hipMemcpyAsync(h, sums + 8, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        if (int e = comm_sync(cm, st, "the m_comp all-reduce")) return e;
+        if (int e = comm_fetch(cm, st, h, sums + 8, 2 * sizeof(int64_t), "the m_comp all-reduce")) return e;
         stats->m_comp = h[0];
         stats->reached = h[1];
     }

@@ -134,8 +134,8 @@ int bfs_validate(bfsx_graph *g, int64_t source, const unsigned long long *stt, i
                        nglob, source, (u64 *)red.p);
     BFSX_HIP_TRY(hipGetLastError());
     u64 h[4];
-    BFSX_HIP_TRY(hipMemcpyAsync(h, red.p, sizeof(h), hipMemcpyDeviceToHost, st));
-    BFSX_HIP_TRY(hipStreamSynchronize(st));
+    if (int e = comm_fetch(part ? cm : nullptr, st, h, red.p, sizeof(h), "the validation's distance all-gather"))
+        return e;
     res[0] = (int64_t)h[0];
     res[1] = h[1] == ~0ull ? -1 : (int64_t)h[1];
     res[2] = (int64_t)h[2];
@@ -152,11 +152,7 @@ int bfs_validate(bfsx_graph *g, int64_t source, const unsigned long long *stt, i
         v[3 + g->rank] = res[1] + 1; // 0 = none
         BFSX_HIP_TRY(hipMemcpyAsync(d, v.data(), v.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
         int e = cm->allreduce_sum(d, (int)v.size(), st);
-        if (!e) {
-            hipError_t he = hipMemcpyAsync(v.data(), d, v.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st);
-            if (he == hipSuccess) he = hipStreamSynchronize(st);
-            if (he != hipSuccess) e = fail(BFSX_E_HIP, std::string("validate: ") + hipGetErrorString(he));
-        }
+        if (!e) e = comm_fetch(cm, st, v.data(), d, v.size() * sizeof(int64_t), "the validation's all-reduce");
         (void)hipFree(d);
         if (e) return e;
         res[0] = v[0];
