@@ -489,7 +489,13 @@ int comm_fetch(Comm *cm, hipStream_t st, void *dst, const void *d_src, size_t by
         cm->pinned_bytes = cap;
     }
     BFSX_HIP_TRY(hipMemcpyAsync(cm->pinned, d_src, bytes, hipMemcpyDeviceToHost, st));
-    if (int e = comm_sync(cm, st, what)) return e;
+    if (int e = comm_sync(cm, st, what)) {
+        // the copy may still be queued behind the failed collective: the buffer is left to it (a few KiB
+        // leaked once per failed communicator) instead of being freed under a pending transfer
+        cm->pinned = nullptr;
+        cm->pinned_bytes = 0;
+        return e;
+    }
     std::memcpy(dst, cm->pinned, bytes);
     return BFSX_OK;
 }
