@@ -533,7 +533,8 @@ def run_dist(args, world, rank, local_rank):
     import torch.distributed as dist
 
     arm_deadline(args.deadline, f"rank {rank} of {world}")
-    if os.environ.get("BFSX_RCCL_SHARED_DEVICE") == "1":
+    shared_device = os.environ.get("BFSX_RCCL_SHARED_DEVICE") == "1"
+    if shared_device:
         # rehearsal of N > 1 RCCL on a box with fewer GPUs than ranks: RCCL refuses two ranks on one device of
         # one host, so every rank presents a host id of its own and the ranks talk over RCCL's socket transport
         # (loopback). Never set by the driver's runs; see DESIGN §7.
@@ -558,8 +559,18 @@ def run_dist(args, world, rank, local_rank):
     dist.broadcast_object_list(uid, src=0)
     ctx.comm_init(rank, world, uid[0])
     t0 = time.perf_counter()
-    g = ctx.dist_kronecker(args.scale, rank, world, args.edgefactor, args.seed)
-    ctx.synchronize()
+    if shared_device:
+        # ranks sharing one GPU build one after another: the build's temporaries are several times its slice
+        # (four concurrent scale-30 builds do not fit one GPU's 288 GB; on their own GPUs they run at once)
+        g = None
+        for r in range(world):
+            if r == rank:
+                g = ctx.dist_kronecker(args.scale, rank, world, args.edgefactor, args.seed)
+                ctx.synchronize()
+            dist.barrier()
+    else:
+        g = ctx.dist_kronecker(args.scale, rank, world, args.edgefactor, args.seed)
+        ctx.synchronize()
     build_s = time.perf_counter() - t0
     part = g.partition()
     # untimed, collective (m_comp is all-reduced, so every rank keeps the same roots): m_comp and
