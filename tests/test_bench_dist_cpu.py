@@ -78,3 +78,19 @@ def test_bench_deadline_ends_a_stuck_run():
     assert r.returncode != 0 and not r.stdout.strip(), (r.returncode, r.stdout, r.stderr[-3000:])
     assert "deadline of 20 s passed" in r.stderr, r.stderr[-3000:]
     assert took < 150, took
+
+
+def test_bench_shared_device_rehearsal_mode():
+    """BFSX_RCCL_SHARED_DEVICE=1 (the one-GPU RCCL rehearsal): every rank gets its own NCCL_HOSTID and
+    the ranks build their slices one after another; the line is the same as without it."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", BFSX_RCCL_SHARED_DEVICE="1",
+               BFSX_BENCH_BINDING=os.path.join(ROOT, "tests", "bench_dist_fake.py"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--scale", "12", "--roots",
+                        "4", "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["bfs_runs"] == 8
