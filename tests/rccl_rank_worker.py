@@ -55,6 +55,9 @@ def main():
     t00 = time.time()
     bfsx = conftest.load_bfsx()
     opts = {"check_collectives": "on", "comm_timeout_ms": "60000"}
+    for kv in filter(None, os.environ.get("BFSX_WORKER_OPTIONS", "").split(",")):  # extra options, k=v,k=v
+        k, v = kv.split("=", 1)
+        opts[k] = v
     if mode.startswith("fail:"):  # fail:R:LEVEL[:off] -- off: without the collective-sequence check
         f = mode.split(":")
         opts["fail_at"] = f"{f[1]}:{f[2]}"

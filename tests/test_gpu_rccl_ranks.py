@@ -26,13 +26,14 @@ INF = 2147483647
 WORKER = os.path.join(ROOT, "tests", "rccl_rank_worker.py")
 
 
-def launch(tmp_path, world, mode, scale, seed, sources, limit=150):
+def launch(tmp_path, world, mode, scale, seed, sources, limit=150, options=None):
     """Start the P rank processes (each its own NCCL_HOSTID), wait for all of them against one deadline."""
     uid = str(tmp_path / "rccl.uid")
     procs = []
     for r in range(world):
         env = dict(os.environ, NCCL_HOSTID=f"bfsx-test-rank{r}", NCCL_SOCKET_IFNAME="lo",
-                   BFSX_WORKER_STACK_AFTER=str(limit - 20))
+                   BFSX_WORKER_STACK_AFTER=str(limit - 20),
+                   BFSX_WORKER_OPTIONS=",".join(f"{k}={v}" for k, v in (options or {}).items()))
         env.pop("BFSX_RCCL_SHARED_DEVICE", None)
         cmd = [sys.executable, WORKER, str(r), str(world), uid, str(tmp_path / f"rank{r}"), mode, str(scale),
                hex(seed), ",".join(str(s) for s in sources)]
@@ -50,13 +51,19 @@ def launch(tmp_path, world, mode, scale, seed, sources, limit=150):
     return tails
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_rccl_ranks_parity(tmp_path, world):
+@pytest.mark.parametrize("world,options", [
+    (2, {}), (4, {}),
+    # every push level through the counted exchange (count all-to-all, then the pair all-to-allv)
+    (2, {"slot_pairs": "0"}), (4, {"slot_pairs": "0"}),
+    # every pull level after the first receives the frontier as id lists (all-to-allv) instead of the all-gather
+    (2, {"sparse_exchange": "on"}), (4, {"sparse_exchange": "on", "direction": "bottomup"}),
+])
+def test_rccl_ranks_parity(tmp_path, world, options):
     scale, seed = 15, 0x2CC1
     u, v = O.kronecker(scale, 16, seed)
     nv = 1 << scale
     sources = [int(u[0]), int(u[4321]), int(v[99])]
-    launch(tmp_path, world, "parity", scale, seed, sources)
+    launch(tmp_path, world, "parity", scale, seed, sources, options=options)
     res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     off, col = O.build_sets(nv, u, v)
     for i, s in enumerate(sources):
