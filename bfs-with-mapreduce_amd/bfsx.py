@@ -16,7 +16,8 @@ LIB_PATH = os.environ.get("BFSX_LIB") or os.path.join(PKG_DIR, "libbfsx.so")
 # the diagnostic build of the same sources (-DBFSX_DIAG): the test hooks and the encoded hub domain of graphs
 # built without the relabel; a Context given one of DIAG_OPTIONS (or diag=True) runs on it
 DIAG_LIB_PATH = os.environ.get("BFSX_DIAG_LIB") or os.path.join(PKG_DIR, "libbfsx_diag.so")
-DIAG_OPTIONS = ("poison_queues", "test_overread", "bu_force_spill", "persist_abort_at", "check_retired", "fail_at")
+DIAG_OPTIONS = ("poison_queues", "test_overread", "bu_force_spill", "persist_abort_at", "check_retired", "fail_at",
+                "slot_force", "race_probe")
 
 BFSX_OK = 0
 BFSX_E_IO = -1

@@ -392,6 +392,32 @@ __device__ inline void publish_if_last(LevelSlot *slot, Published *pub, u64 seq)
     }
 }
 
+// ---- store guards (round 6) ----------------------------------------------------------------------
+// Every computed global index of the push / exchange path is checked against its buffer's capacity before the
+// store.  A violation is not written: it is reported in the workspace's mapped error words (err[0] = 2 << 32 |
+// site, err[1] = index, err[2] = bound) and fails the BFS -- on a partition at the level close, on every rank
+// together (level_sums' guard bit) -- instead of becoming a wild store.  One compare per flush or per pair.
+enum GuardSite : uint32_t {
+    kSiteSlot = 1,     // rq_flush: a pair's position in its destination's fixed exchange slot
+    kSiteSlotDest = 2, // rq_flush / bucketing: a pair's destination rank
+    kSiteRemote = 3,   // rq_flush: the counted exchange's remote-pair buffer
+    kSiteHubs = 4,     // k_td: the hub list
+    kSiteQueue = 5,    // q_flush: the next-frontier queue / push-log segment
+    kSiteBucket = 6,   // k_bucket_scatter: the send buffer
+};
+constexpr int kErrWords = 4; // mapped error words: [0] code, [1] index, [2] bound
+__device__ inline bool idx_ok(u64 i, u64 bound, u64 *err, uint32_t site) {
+    if (i < bound) return true;
+    if (err) {
+        volatile u64 *e = reinterpret_cast<volatile u64 *>(err);
+        e[1] = i;
+        e[2] = bound;
+        __threadfence_system();
+        e[0] = 0x200000000ull | site;
+    }
+    return false;
+}
+
 // ---- block-level output queue ------------------------------------------------------------------
 // Winners are appended to an LDS buffer (LDS atomics) and flushed to the global next-frontier queue
 // with ONE global atomic per flush (~kQCap winners): a single device counter hit by every wave
@@ -469,17 +495,22 @@ __device__ inline void q_push(LogQueueT<C> &q, bool win, uint32_t v, uint32_t pa
     if (win) q.buf[base + __popcll(mask & ((1ull << lane) - 1ull))] = (u64)v | ((u64)parent << 32);
 }
 template <int C>
-__device__ inline void q_flush(BlockQueueT<C> &q, uint32_t *__restrict__ qout, u64 *, u64 *qtail) {
+__device__ inline void q_flush(BlockQueueT<C> &q, uint32_t *__restrict__ qout, u64 *, u64 *qtail, u64 = ~0ull,
+                               u64 * = nullptr) {
     bq_flush(q, qout, qtail);
 }
+// qcap / err: the entries the output queue (and the push-log segment) hold; a flush that would pass them is
+// reported (kSiteQueue) and dropped instead of written
 template <int C>
-__device__ inline void q_flush(LogQueueT<C> &q, uint32_t *__restrict__ qout, u64 *__restrict__ plog, u64 *qtail) {
+__device__ inline void q_flush(LogQueueT<C> &q, uint32_t *__restrict__ qout, u64 *__restrict__ plog, u64 *qtail,
+                               u64 qcap = ~0ull, u64 *err = nullptr) {
     const uint32_t n = q.n;
     if (n == 0) return;
     if (threadIdx.x == 0) q.gbase = (uint32_t)atomicAdd(qtail, (u64)n);
     __syncthreads();
     const uint32_t gb = q.gbase;
-    for (uint32_t i = threadIdx.x; i < n; i += kBS) {
+    if (lane_id() == 0) (void)idx_ok((u64)gb + n - 1u, qcap, err, kSiteQueue); // every wave checks what it stores
+    for (uint32_t i = threadIdx.x; i < n && (u64)gb + n <= qcap; i += kBS) {
         const u64 e = q.buf[i];
         qout[gb + i] = (uint32_t)e;
         if (plog) plog[gb + i] = e;
@@ -527,8 +558,11 @@ struct Part {
     uint32_t nrows;  // rows held here: every queued id must be below it (id_ok)
     u64 *remote;      // (v << 32 | parent) pairs for vertices owned elsewhere
     u64 *remote_tail; // their allocation cursor
+    u64 remote_cap;   // entries `remote` holds (kSiteRemote)
+    u64 qcap;         // entries the push kernels' next-frontier queue and push-log segment hold (kSiteQueue)
     u64 *err;         // mapped host word: set when a queue holds an id >= nrows (null: unchecked)
     uint32_t nranks;
+    uint32_t probe;   // diagnostic build, option race_probe: 1 delay, 2 delay + no queue-init barrier (k_td)
     // small partitioned push levels (fixed-slot exchange): remote pairs go straight into the send buffer's
     // per-destination slots [count, slot_cap pairs] (slot_cap 0: into `remote` for the counted exchange);
     // the level's last push kernel has slot_arrive set: its last workgroup writes the slot counts
@@ -580,12 +614,13 @@ __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
         constexpr int kPer = kRCap / kBS;
         for (int d = threadIdx.x; d < kMaxRanks; d += kBS) q.h[d] = 0u;
         __syncthreads();
-        uint32_t r[kPer], dst[kPer];
+        uint32_t r[kPer], dst[kPer]; // dst = kMaxRanks: no slot (past the queue, or a guarded destination)
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const uint32_t i = threadIdx.x + (uint32_t)k * kBS;
-            dst[k] = i < n ? (uint32_t)(q.buf[i] >> 32) / pt.chunk : 0u;
-            r[k] = i < n ? atomicAdd(&q.h[dst[k]], 1u) : 0u;
+            const uint32_t d = i < n ? (uint32_t)(q.buf[i] >> 32) / pt.chunk : 0u;
+            dst[k] = (i < n && idx_ok(d, pt.nranks, pt.err, kSiteSlotDest)) ? d : (uint32_t)kMaxRanks;
+            r[k] = dst[k] < (uint32_t)kMaxRanks ? atomicAdd(&q.h[dst[k]], 1u) : 0u;
         }
         __syncthreads();
         for (int d = threadIdx.x; d < kMaxRanks; d += kBS)
@@ -594,7 +629,9 @@ __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const uint32_t i = threadIdx.x + (uint32_t)k * kBS;
-            if (i < n) pt.slot_out[(u64)dst[k] * (pt.slot_cap + 1) + 1 + q.base[dst[k]] + r[k]] = q.buf[i];
+            // the slot bound is the host's per-peer bound on this level's pairs (the global m_f, kernels_dist.hip)
+            if (dst[k] < (uint32_t)kMaxRanks && idx_ok(q.base[dst[k]] + r[k], pt.slot_cap, pt.err, kSiteSlot))
+                pt.slot_out[(u64)dst[k] * (pt.slot_cap + 1) + 1 + q.base[dst[k]] + r[k]] = q.buf[i];
         }
         __syncthreads();
         if (threadIdx.x == 0) q.n = 0;
@@ -604,7 +641,9 @@ __device__ inline void rq_flush(RemoteQueue &q, const Part &pt) {
     if (threadIdx.x == 0) q.gbase = atomicAdd(pt.remote_tail, (u64)n);
     __syncthreads();
     const u64 gb = q.gbase;
-    for (uint32_t i = threadIdx.x; i < n; i += kBS) pt.remote[gb + i] = q.buf[i];
+    // the remote buffer holds the local frontier's m_f pairs (the host's bound, kernels_dist.hip)
+    if (lane_id() == 0) (void)idx_ok(gb + n - 1u, pt.remote_cap, pt.err, kSiteRemote);
+    for (uint32_t i = threadIdx.x; i < n && gb + n <= pt.remote_cap; i += kBS) pt.remote[gb + i] = q.buf[i];
     __syncthreads();
     if (threadIdx.x == 0) q.n = 0;
     __syncthreads();

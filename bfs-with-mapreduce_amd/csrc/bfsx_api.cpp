@@ -395,7 +395,8 @@ static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
 #ifndef BFSX_DIAG
     // test hooks and diagnostics exist in the diagnostic library only (libbfsx_diag.so, built with BFSX_DIAG);
     // "off" is accepted (a no-op) so that a caller resetting them needs no special case
-    for (const char *d : {"poison_queues", "test_overread", "bu_force_spill", "persist_abort_at", "check_retired", "fail_at"})
+    for (const char *d : {"poison_queues", "test_overread", "bu_force_spill", "persist_abort_at", "check_retired", "fail_at",
+                          "slot_force", "race_probe"})
         if (k == d) {
             if (v == "off") return BFSX_OK;
             return fail(BFSX_E_ARG, k + " is a test hook of the diagnostic library (libbfsx_diag.so, built with "
@@ -560,6 +561,24 @@ static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
         }
         ctx->opt.fail_rank = (int)r;
         ctx->opt.fail_level = (int)lv;
+        return BFSX_OK;
+    }
+    if (k == "race_probe") { // test hook
+        if (v == "off") ctx->opt.race_probe = 0;
+        else if (v == "delay") ctx->opt.race_probe = 1;
+        else if (v == "nobarrier") ctx->opt.race_probe = 2;
+        else return fail(BFSX_E_ARG, "race_probe must be off|delay|nobarrier");
+        return BFSX_OK;
+    }
+    if (k == "slot_force") { // test hook: "off" or a slot size in pairs
+        if (v == "off") {
+            ctx->opt.slot_force = -1;
+            return BFSX_OK;
+        }
+        char *end = nullptr;
+        const long long x = strtoll(value, &end, 10);
+        if (!end || *end || x < 1) return fail(BFSX_E_ARG, "slot_force must be off or a pair count >= 1");
+        ctx->opt.slot_force = x;
         return BFSX_OK;
     }
     if (k == "leaf_skip") {

@@ -69,6 +69,8 @@ struct Options {
     int64_t comm_timeout_ms = 120000; // partitioned path: a host wait on the peers fails after this long
     bool check_collectives = false;   // debug: every collective checks that all ranks are in the same (op, level)
     int fail_rank = -1, fail_level = -1; // test hook (fault injection): that rank fails at that level of the loop
+    int race_probe = 0;         // test hook: k_td's queue init late behind stale LDS (1), and without its barrier (2)
+    int64_t slot_force = -1;    // test hook: fixed-slot push levels use slots of this many pairs (the store guard fires)
 };
 
 // ---- bfsx_comm.cpp: exchange layer of the partitioned BFS ---------------------------------

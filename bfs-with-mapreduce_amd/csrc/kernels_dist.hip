@@ -15,7 +15,8 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
                                                       u64 *__restrict__ stt, uint32_t *__restrict__ qout,
                                                       LevelSlot *ring, int level, uint32_t lo, u64 slot,
                                                       uint32_t nrows, u64 *err, int64_t *sums, u64 *ctr, int nctr,
-                                                      u64 *arrive, int rank, int nranks, u64 *__restrict__ plog) {
+                                                      u64 *arrive, int rank, int nranks, u64 *__restrict__ plog,
+                                                      u64 qcap) {
     LevelSlot *cn = ring + (level + 1) % 3;
     __shared__ LogQueue q; // plog (the push log's segment of this level): winners as (vertex, parent) pairs
     using Q = LogQueue;
@@ -51,9 +52,9 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
         }
         q_push(q, win, vl, parent);
         __syncthreads();
-        if (q.n > Q::kCap - (uint32_t)kBS) q_flush(q, qout, plog, &cn->qtail);
+        if (q.n > Q::kCap - (uint32_t)kBS) q_flush(q, qout, plog, &cn->qtail, qcap, err);
     }
-    q_flush(q, qout, plog, &cn->qtail);
+    q_flush(q, qout, plog, &cn->qtail, qcap, err);
     shard_add(cn, 0, acc_mf, 0, attempts, 0, acc_dmax);
     if (!sums) return;
     // the level close in the last workgroup to arrive (no k_level_sums dispatch): every wave's queue and
@@ -72,14 +73,19 @@ __global__ __launch_bounds__(kBS) void k_claim_remote(const u64 *__restrict__ pa
 // (workgroup, destination) and LDS-ranked scatter.
 
 
+// n_cap: the pairs `pairs` holds (a tail past it was guarded by rq_flush and is not read); a pair whose destination
+// is not a rank is reported (kSiteSlotDest) and left out.
 __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
-                                                      uint32_t chunk, int nranks, u64 *__restrict__ dcount) {
+                                                      u64 n_cap, uint32_t chunk, int nranks, u64 *__restrict__ dcount,
+                                                      u64 *err) {
     __shared__ uint32_t s_h[kMaxRanks];
-    const uint64_t n = *d_n;
+    const uint64_t n = min(*d_n, n_cap);
     for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS)
-        atomicAdd(&s_h[(uint32_t)(pairs[i] >> 32) / chunk], 1u);
+    for (uint64_t i = (uint64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBS) {
+        const uint32_t d = (uint32_t)(pairs[i] >> 32) / chunk;
+        if (idx_ok(d, (u64)nranks, err, kSiteSlotDest)) atomicAdd(&s_h[d], 1u);
+    }
     __syncthreads();
     for (int d = threadIdx.x; d < nranks; d += kBS)
         if (s_h[d]) atomicAdd(&dcount[d], (u64)s_h[d]);
@@ -89,21 +95,24 @@ __global__ __launch_bounds__(kBS) void k_bucket_count(const u64 *__restrict__ pa
 // all-to-all and no host round trip before the pairs move) are bucketed by the push kernels themselves
 // (rq_flush in slot mode, slot_headers_if_last); the counted exchange below buckets in two passes.
 __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ pairs, const u64 *__restrict__ d_n,
-                                                        uint32_t chunk, int nranks, const u64 *__restrict__ dcount,
-                                                        u64 *__restrict__ dcursor, u64 *__restrict__ out) {
+                                                        u64 n_cap, uint32_t chunk, int nranks,
+                                                        const u64 *__restrict__ dcount, u64 *__restrict__ dcursor,
+                                                        u64 *__restrict__ out, u64 out_cap, u64 *err) {
     __shared__ uint32_t s_h[kMaxRanks];
     __shared__ u64 s_base[kMaxRanks];
-    const uint64_t n = *d_n;
+    const uint64_t n = min(*d_n, n_cap);
     for (uint64_t i0 = (uint64_t)blockIdx.x * kBS; i0 < n; i0 += (uint64_t)gridDim.x * kBS) {
         for (int d = threadIdx.x; d < nranks; d += kBS) s_h[d] = 0;
         __syncthreads();
         const uint64_t i = i0 + threadIdx.x;
         u64 pr = 0;
         uint32_t d = 0, r = 0;
+        bool ok = false;
         if (i < n) {
             pr = pairs[i];
             d = (uint32_t)(pr >> 32) / chunk;
-            r = atomicAdd(&s_h[d], 1u);
+            ok = d < (uint32_t)nranks; // reported by k_bucket_count
+            if (ok) r = atomicAdd(&s_h[d], 1u);
         }
         __syncthreads();
         for (int k = threadIdx.x; k < nranks; k += kBS) {
@@ -114,7 +123,7 @@ __global__ __launch_bounds__(kBS) void k_bucket_scatter(const u64 *__restrict__ 
             }
         }
         __syncthreads();
-        if (i < n) out[s_base[d] + r] = pr;
+        if (ok && idx_ok(s_base[d] + r, out_cap, err, kSiteBucket)) out[s_base[d] + r] = pr;
         __syncthreads();
     }
 }
@@ -143,6 +152,17 @@ __global__ __launch_bounds__(kBS) void k_ids_to_bitmap(const u64 *__restrict__ i
         atomicOr(bm + (v >> 6), 1ull << (v & 63u));
     }
 }
+
+#ifdef BFSX_DIAG
+// Option race_probe (diagnostic): fill the LDS of every CU with 0x01010101 words, so that a push workgroup reading its
+// queue counts before they are zeroed reads 16,843,009 (event (d)).
+__global__ __launch_bounds__(kBS) void k_lds_poison() {
+    __shared__ uint32_t s[8192]; // 32 KiB; several resident workgroups per CU cover its LDS
+    for (int i = threadIdx.x; i < 8192; i += kBS) s[i] = 0x01010101u;
+    __syncthreads();
+    if (s[threadIdx.x ^ 1] == 0u) s[0] = 1u; // keeps the stores
+}
+#endif
 
 // Multi-GPU host reads without a D2H copy + stream synchronise: one wave copies two device ranges into
 // mapped pinned host memory and then publishes a sequence number the host spins on (as publish_if_last).
@@ -205,6 +225,7 @@ inline Part make_part(bfsx_graph *g, BfsWorkspace *ws) {
     p.rank = (uint32_t)g->rank;
     p.remote = ws->remote;
     p.remote_tail = ws->d_dist_ctr;
+    p.remote_cap = (u64)ws->remote_cap;
     p.nrows = (uint32_t)g->nv;
     p.err = ws->d_err;
     p.nranks = (uint32_t)g->nranks;
@@ -342,10 +363,11 @@ int dist_td_expand(bfsx_graph *g, u64 *d_send, int64_t send_cap, int64_t *send_c
     if (n_remote > 0) {
         const unsigned gbk = clamp_grid(((int64_t)n_remote + kBS - 1) / kBS, 1024);
         hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                           (uint32_t)g->chunk, P, dcount);
+                           (u64)ws->remote_cap, (uint32_t)g->chunk, P, dcount, ws->d_err);
         BFSX_LAUNCHED(st);
         hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                           (uint32_t)g->chunk, P, dcount, dcursor, d_send);
+                           (u64)ws->remote_cap, (uint32_t)g->chunk, P, dcount, dcursor, d_send, (u64)send_cap,
+                           ws->d_err);
         BFSX_LAUNCHED(st);
     }
     std::vector<u64> h(P, 0);
@@ -366,11 +388,11 @@ int dist_td_claim(bfsx_graph *g, const u64 *d_recv, int64_t n) {
     if (ws->off32)
         hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, ws->off32, ws->vis,
                            ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
-                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks, nullptr);
+                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks, nullptr, (u64)g->nv);
     else
         hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, d_recv, (u64)n, g->d_row_off,
                            ws->vis, ws->st, ws->qb, ws->ring, ws->d_level, (uint32_t)g->v_lo, (u64)0, (uint32_t)g->nv, ws->d_err,
-                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks, nullptr);
+                           nullptr, nullptr, 0, nullptr, g->rank, g->nranks, nullptr, (u64)g->nv);
     BFSX_LAUNCHED(st);
     return BFSX_OK;
 }
@@ -497,7 +519,7 @@ void trace_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level) {
              {"remote", ws->remote, ws->remote_cap * 8}, {"sendbuf", ws->sendbuf, ws->send_cap * 8},
              {"recvbuf", ws->recvbuf, ws->recv_cap * 8}, {"fglob", ws->fglob, ws->fglob_words * 8},
              {"dist_ctr", ws->d_dist_ctr, kCtrWords * 8}, {"post", ws->d_post, kPostWords * 8},
-             {"err", ws->d_err, 8},                      {"pub", ws->d_pub, (int64_t)sizeof(Published)}};
+             {"err", ws->d_err, kErrWords * 8},                   {"pub", ws->d_pub, (int64_t)sizeof(Published)}};
     for (const auto &x : b)
         fprintf(stderr, "[bfsx] rank %d level %d buffer %-8s [0x%llx, 0x%llx)\n", g->rank, level, x.name,
                 (unsigned long long)(uintptr_t)x.p, (unsigned long long)((uintptr_t)x.p + x.bytes));
@@ -782,6 +804,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                 // kernels write the pairs into the slots themselves; the last one's last workgroup writes the
                 // counts (dcount, unused by the slot exchange, counts its arrivals)
                 slot = std::max<int64_t>(mf, 1);
+                if (BFSX_DIAG_ON && opt.slot_force > 0) slot = opt.slot_force; // test hook: a slot bound too small
                 if (int e = grow(ws, ws->sendbuf, ws->send_cap, P * (slot + 1))) return e;
                 if (int e = grow(ws, ws->recvbuf, ws->recv_cap, P * (slot + 1))) return e;
                 pt.slot_out = ws->sendbuf;
@@ -799,14 +822,22 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
             // the push log (option push_log, as on one device): this level's winners, local claims and remote ones
             // alike, are (vertex, parent) pairs at their queue positions in the log segment [log_n, log_n + n_f)
             plog = opt.push_log ? ws->plog + ws->log_n : nullptr;
+#ifdef BFSX_DIAG
+            if (opt.race_probe) { // test hook: stale LDS + a late queue init (k_td)
+                hipLaunchKernelGGL(k_lds_poison, dim3(g->ctx->num_cus * 8), dim3(kBS), 0, st);
+                BFSX_LAUNCHED(st);
+                pt.probe = (uint32_t)opt.race_probe;
+            }
+#endif
             if (int e = launch_td<true>(g, ws, nq, ws->d_mf, dmax_local, level, pt, false, nullptr, 0, nullptr, plog))
                 return e;
             if (!slot) {
                 hipLaunchKernelGGL(k_bucket_count, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                                   (uint32_t)g->chunk, P, dcount);
+                                   (u64)ws->remote_cap, (uint32_t)g->chunk, P, dcount, ws->d_err);
                 BFSX_LAUNCHED(st);
                 hipLaunchKernelGGL(k_bucket_scatter, dim3(gbk), dim3(kBS), 0, st, ws->remote, ws->d_dist_ctr,
-                                   (uint32_t)g->chunk, P, dcount, dcursor, ws->sendbuf);
+                                   (u64)ws->remote_cap, (uint32_t)g->chunk, P, dcount, dcursor, ws->sendbuf,
+                                   (u64)ws->send_cap, ws->d_err);
                 BFSX_LAUNCHED(st);
                 u64 *drecv = ws->d_dist_ctr + kCtrRecv;
                 if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
@@ -825,17 +856,18 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                 return e;
             if (ro > 0) { // its last workgroup closes the level (the sums k_level_sums would compute)
                 const dim3 grid(clamp_grid((ro + kBS - 1) / kBS, cap));
+                const u64 qcap = (u64)std::max<int64_t>(plog ? g->nv - ws->log_n : g->nv, 0); // as the push kernels'
                 u64 *arrive = ws->d_dist_ctr + kCtrHead - 1;
                 if (ws->off32)
                     hipLaunchKernelGGL(k_claim_remote<uint32_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        ws->off32, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
                                        (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive,
-                                       g->rank, g->nranks, plog);
+                                       g->rank, g->nranks, plog, qcap);
                 else
                     hipLaunchKernelGGL(k_claim_remote<int64_t>, grid, dim3(kBS), 0, st, ws->recvbuf, (u64)ro,
                                        g->d_row_off, ws->vis, ws->st, ws->qb, ws->ring, level, (uint32_t)g->v_lo,
                                        (u64)slot, (uint32_t)g->nv, ws->d_err, sums, ws->d_dist_ctr, kCtrHead, arrive,
-                                       g->rank, g->nranks, plog);
+                                       g->rank, g->nranks, plog, qcap);
                 BFSX_LAUNCHED(st);
                 summed = true;
             }
@@ -917,7 +949,8 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
             std::string mine;
             if (check_queue_guard(ws)) mine = " (this rank: " + last_error() + ")";
             cm->agreed = true; // every rank leaves here with this error: the communicator stays usable
-            return fail(BFSX_E_HIP, "queue guard fired at level " + std::to_string(level) + " on rank(s) " + who + mine);
+            return fail(BFSX_E_HIP, "device guard (queue id / store bound) fired at level " + std::to_string(level) +
+                                        " on rank(s) " + who + mine);
         }
         static const bool trace = std::getenv("BFSX_TRACE") != nullptr;
         if (trace)

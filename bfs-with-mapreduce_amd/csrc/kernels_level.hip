@@ -457,9 +457,9 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipHostMalloc(&ws->h_pub, sizeof(Published), hipHostMallocMapped | hipHostMallocCoherent));
     BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&ws->d_pub, ws->h_pub, 0));
     ws->h_pub->seq = 0;
-    BFSX_HIP_TRY(hipHostMalloc(&ws->h_err, sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent));
+    BFSX_HIP_TRY(hipHostMalloc(&ws->h_err, kErrWords * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent));
     BFSX_HIP_TRY(hipHostGetDevicePointer((void **)&ws->d_err, ws->h_err, 0));
-    *ws->h_err = 0;
+    for (int i = 0; i < kErrWords; i++) ws->h_err[i] = 0;
     BFSX_HIP_TRY(hipMalloc(&ws->d_cursor, sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->d_red, 3 * sizeof(u64)));
     BFSX_HIP_TRY(hipEventCreate(&ws->ev_start));
@@ -509,12 +509,24 @@ Part single_part(const bfsx_graph *g, const BfsWorkspace *ws) {
     return p;
 }
 
-// After a BFS: fail if a queue consumer met an out-of-range id (the word is cleared for the next BFS).
+// After a BFS (a partition: at every level close): fail if a queue consumer met an out-of-range id (id_ok) or a
+// store guard refused an index (idx_ok); the words are cleared for the next BFS.
 int check_queue_guard(BfsWorkspace *ws) {
     std::atomic_thread_fence(std::memory_order_acquire);
-    const u64 e = *reinterpret_cast<volatile u64 *>(ws->h_err);
+    volatile u64 *w = reinterpret_cast<volatile u64 *>(ws->h_err);
+    const u64 e = w[0], idx = w[1], bound = w[2];
     if (!e) return BFSX_OK;
-    *reinterpret_cast<volatile u64 *>(ws->h_err) = 0;
+    for (int i = 0; i < kErrWords; i++) w[i] = 0;
+    if ((e >> 32) == 2u) {
+        static const char *const site[] = {"?", "a fixed exchange slot (pairs routed to one peer)",
+                                           "the destination rank of a routed pair", "the remote-pair buffer",
+                                           "the hub list", "the next-frontier queue / push-log segment",
+                                           "the pair send buffer"};
+        const uint32_t s = (uint32_t)e;
+        return fail(BFSX_E_HIP, std::string("internal error: store guard: index ") + std::to_string(idx) +
+                                    " into " + (s < 7 ? site[s] : "?") + " of bound " + std::to_string(bound) +
+                                    " refused (a host bound was too small; nothing was written)");
+    }
     return fail(BFSX_E_HIP, "internal error: a frontier-queue consumer read vertex id " +
                                 std::to_string((uint32_t)e) + ", outside the rows of this graph (stale queue entry)");
 }

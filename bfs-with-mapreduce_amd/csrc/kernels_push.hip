@@ -79,7 +79,7 @@ __device__ inline void sweep_segments(const ScanT *s_scan, const BegT *s_beg, co
             if (kDist) rq_push(*rq, send, ((u64)v[k] << 32) | pu[k]);
         }
         __syncthreads();
-        if (q.n > Q::kCap - (uint32_t)(kBS * kItems)) q_flush(q, qout, plog, qtail);
+        if (q.n > Q::kCap - (uint32_t)(kBS * kItems)) q_flush(q, qout, plog, qtail, pt.qcap, pt.err);
         if (kDist && rq->n > (uint32_t)(kRCap - kBS * kItems)) rq_flush(*rq, pt);
     }
 }
@@ -101,8 +101,17 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
     __shared__ typename std::conditional<kDist, DistQueue, LogQueue>::type q;
     __shared__ typename std::conditional<kDist, RemoteQueue, char>::type rq_storage;
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
+    if (BFSX_DIAG_ON && pt.probe && threadIdx.x < 64) // option race_probe: wave 0 zeroes the counts late
+        for (int i = 0; i < 64; i++) __builtin_amdgcn_s_sleep(127);
     bq_init(q);
     if (kDist && threadIdx.x == 0) rq->n = 0;
+    // Every wave must see the zeroed queue counts before it reads them.  A workgroup with no frontier vertex (a
+    // partitioned rank whose local frontier is empty: every non-owner at level 0) goes straight to the final
+    // flushes; without this barrier waves 1-3 could read q.n / rq->n before wave 0 zeroed them -- whatever an
+    // earlier kernel left in that LDS -- and flush that many stale entries to a stale base: the round-3..5
+    // "illegal memory access" of the partitioned push levels (event (d)).
+    if (!(BFSX_DIAG_ON && pt.probe == 2)) __syncthreads(); // race_probe=nobarrier: the rounds-3..5 code
+
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     u64 acc_mf = 0, attempts = 0, scanned = 0, acc_dmax = 0, acc_mfh = 0, acc_nh = 0, acc_ex = 0;
@@ -124,7 +133,8 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
             } else if (is_hub(skip, u + pt.lo, (u64)d)) { // hybrid level: the pull hub sweep covers this vertex
                 d = 0;
             } else if (d > (int64_t)hub_deg) {
-                hubs[atomicAdd(&cn->nhub, 1ull)] = u;
+                const u64 h = atomicAdd(&cn->nhub, 1ull); // the list holds nrows ids (a vertex is queued once)
+                if (idx_ok(h, pt.nrows, pt.err, kSiteHubs)) hubs[h] = u;
                 d = 0;
             }
             deg = (uint32_t)d;
@@ -151,7 +161,7 @@ __global__ __launch_bounds__(kBS) void k_td(const OffT *__restrict__ row_off, co
                               rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, acc_ex, plog);
         __syncthreads();
     }
-    q_flush(q, qout, plog, &cn->qtail);
+    q_flush(q, qout, plog, &cn->qtail, pt.qcap, pt.err);
     if (kDist) rq_flush(*rq, pt);
     // top-down: stage2 = degree sum of the hub-domain vertices discovered, walked = their number
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh, acc_ex);
@@ -189,7 +199,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
     RemoteQueue *rq = kDist ? reinterpret_cast<RemoteQueue *>(&rq_storage) : nullptr;
     bq_init(q);
     if (kDist && threadIdx.x == 0) rq->n = 0;
-    const uint32_t nh = (uint32_t)cn->nhub;
+    const uint32_t nh = (uint32_t)min(cn->nhub, (u64)pt.nrows); // k_td's guard dropped any entry past nrows
     const int32_t nd = level + 1;
     const unsigned tid = threadIdx.x;
     constexpr int kPer = kHubBatch / kBS;
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(kBS) void k_td_hubs(const OffT *__restrict__ row_of
                               &cn->qtail, pt, rq, acc_mf, attempts, acc_dmax, hs, acc_mfh, acc_nh, acc_ex, plog, s_vp, vpref);
         __syncthreads();
     }
-    q_flush(q, qout, plog, &cn->qtail);
+    q_flush(q, qout, plog, &cn->qtail, pt.qcap, pt.err);
     if (kDist) rq_flush(*rq, pt);
     shard_add(cn, 0, acc_mf, scanned, attempts, 0, acc_dmax, acc_mfh, acc_nh, acc_ex);
     publish_if_last(cn, pub, seq);
@@ -270,8 +280,11 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
     // hubs: sized by the frontier's degree sum when known (mf < 0: after a bottom-up level)
     const bool hubs = dmax >= 0 ? dmax > (int64_t)hub_deg : (mf < 0 || mf > (int64_t)hub_deg);
     const dim3 gh(mf < 0 ? cap : clamp_grid((mf + kBS * kItems - 1) / (kBS * kItems), cap));
+    // the next-frontier queue holds nv ids; the push-log segment [log_n, nv) what is left of the log
+    Part ptq = pt;
+    ptq.qcap = (u64)std::max<int64_t>(plog ? g->nv - ws->log_n : g->nv, 0);
     // slot mode: only the level's last push kernel writes the slot headers
-    Part pt0 = pt;
+    Part pt0 = ptq;
     if (hubs) pt0.slot_arrive = nullptr;
     // the LDS snapshot of the hubs' visited bits (relabelled single-device graphs: the hubs are the lowest ids)
     const uint32_t vpref = (!kDist && g->d_perm && g->ctx->opt.hub_lds_skip)
@@ -283,7 +296,7 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, uint32_t>), gh, dim3(kBS), 0, st, ws->off32, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, pt, hs, pub, seq, plog, vpref);
+                               ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, ptq, hs, pub, seq, plog, vpref);
             BFSX_LAUNCHED(st);
         }
     } else {
@@ -293,7 +306,7 @@ int launch_td(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t mf, int64_t d
         BFSX_LAUNCHED(st);
         if (hubs) {
             hipLaunchKernelGGL((k_td_hubs<kDist, int64_t>), gh, dim3(kBS), 0, st, g->d_row_off, g->d_col, ws->hubs,
-                               ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, pt, hs, pub, seq, plog, vpref);
+                               ws->qb, ws->vis, ws->st, par, pcode, ws->ring, level, ptq, hs, pub, seq, plog, vpref);
             BFSX_LAUNCHED(st);
         }
     }

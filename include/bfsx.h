@@ -173,7 +173,14 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "check_collectives" = on|off (debug: every collective first checks that all ranks are in the same
  *                 collective of the same level, and fails on every rank with both names otherwise)
  *   "fail_at" = rank:level|rank:setup|off (test hook: that rank of a partitioned BFS fails at the start of that
- *                 level, or before its first collective) */
+ *                 level, or before its first collective)
+ *   "slot_force" = int|off (test hook: the fixed-slot push levels of a partitioned BFS use slots of this many
+ *                 pairs, whatever the level's bound; a too-small slot makes the store guard fail the BFS on
+ *                 every rank instead of writing past the slot)
+ *   "race_probe" = off|delay|nobarrier (test hook: before every partitioned push level the LDS of every CU is
+ *                 filled with stale words and k_td's first wave zeroes its queue counts late; nobarrier also
+ *                 drops the barrier after that init -- the rounds-3..5 kernel, whose empty workgroups then flush
+ *                 stale counts, which the store guard reports) */
 int bfsx_set_option(bfsx_ctx *ctx, const char *key, const char *value);
 
 /* ---- host-only parsing (no device work; usable without a GPU) -------------------------------- */

@@ -526,3 +526,76 @@ def test_group_context_one_call(bfsx, world):
                 g.bfs(1 << 12)  # outside the graph: fails on every rank, and the group stays usable
         with gc.kronecker(12, 16, 1) as g, one.kronecker(12, 16, 1) as g1:
             assert np.array_equal(g.bfs(5)[0], g1.bfs(5)[0])
+
+
+def run_group_errors(bfsx, world, make_graph, source, options):
+    """One partitioned BFS per rank thread; returns every rank's error (None where a rank succeeded)."""
+    opts = dict(GROUP_DEFAULTS, **options)
+    ctxs = [bfsx.Context(0, **opts) for _ in range(world)]
+    graphs = [None] * world
+    try:
+        bfsx.local_group(ctxs)
+        for r in range(world):
+            graphs[r] = make_graph(ctxs[r], r, world)
+        errs = [None] * world
+
+        def work(r):
+            try:
+                graphs[r].dist_bfs(source)
+            except Exception as e:  # noqa: BLE001 -- returned to the test
+                errs[r] = str(e)
+
+        ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        for t in ths:
+            t.start()
+        join_ranks(ths, [e for e in errs if e])
+        return errs
+    finally:
+        for g in graphs:
+            if g is not None:
+                g.free()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_group_store_guard_slot_overflow(bfsx, world):
+    """Round 6 (verdict item 1): every computed index of the push / exchange path is checked before its store.
+    With fixed exchange slots forced to one pair (test hook slot_force), the level-0 owner routes more pairs
+    to a peer than its slot holds: the guard refuses the store, and every rank fails at that level's close
+    with the site, index and bound -- an error, not a device fault."""
+    rng = np.random.default_rng(61 + world)
+    nv = 4000
+    u = rng.integers(0, nv, 8 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 8 * nv).astype(np.uint32)
+    hub = 5  # degree >> world: some peer receives several of its pairs at level 0
+    u = np.r_[u, np.full(nv - 1, hub)].astype(np.uint32)
+    v = np.r_[v, np.delete(np.arange(nv), hub)].astype(np.uint32)
+    errs = run_group_errors(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), hub,
+                            {"slot_force": "1", "direction": "topdown"})
+    assert all(e is not None and "device guard" in e and "fired at level 0" in e for e in errs), errs
+    assert any("store guard" in e and "fixed exchange slot" in e for e in errs), errs
+    # the same graph without the hook: the oracle's distances
+    out = run_group(bfsx, world, lambda c, r, w: c.dist_from_edges(nv, u, v, r, w), [hub], "topdown")
+    check(nv, u, v, [hub], out)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_group_empty_push_workgroup_race(bfsx, world):
+    """DESIGN.md 4, event (d), the cause of the rounds-3..5 intermittent "illegal memory access": a k_td workgroup
+    with no frontier vertex (every non-owner at level 0) went from the queue init straight to its final flushes,
+    and no barrier separated thread 0's zeroing of the LDS queue counts from the other waves' reads.  Test hook
+    race_probe fills every CU's LDS with stale words and makes wave 0 zero the counts late:
+      delay      the product kernel (barrier after the init): the oracle's distances;
+      nobarrier  the rounds-3..5 kernel: the empty workgroup's other waves flush 16,843,009 stale entries to a
+                 stale base -- once a wild store, now refused by the store guard on every rank."""
+    rng = np.random.default_rng(71 + world)
+    nv = 6000
+    u = rng.integers(0, nv, 5 * nv).astype(np.uint32)
+    v = rng.integers(0, nv, 5 * nv).astype(np.uint32)
+    make = lambda c, r, w: c.dist_from_edges(nv, u, v, r, w)  # noqa: E731
+    out = run_group(bfsx, world, make, [0, nv - 1], "auto", {"race_probe": "delay"})
+    check(nv, u, v, [0, nv - 1], out)
+    errs = run_group_errors(bfsx, world, make, 0, {"race_probe": "nobarrier"})
+    assert all(e is not None and "device guard" in e for e in errs), errs
+    assert any("store guard" in e for e in errs), errs
