@@ -1088,10 +1088,11 @@ static int sample_roots_impl(bfsx_graph *g, int count, uint64_t seed, int64_t *r
             }
         }
         if (part) {
-            BFSX_HIP_TRY(hipMemcpyAsync(flag.p, &ok, sizeof(ok), hipMemcpyHostToDevice, st));
+            // fills, not pageable copies: neither may block the host behind a collective a failed peer never joins
+            BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)flag.p, (int)ok, 1, st));
+            BFSX_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)((uint32_t *)flag.p + 1), 0, 1, st));
             if (int e = cm->allreduce_sum(flag.p, 1, st)) return e;
-            BFSX_HIP_TRY(hipMemcpyAsync(&ok, flag.p, sizeof(ok), hipMemcpyDeviceToHost, st));
-            if (int e = comm_sync(cm, st, "root sampling")) return e;
+            if (int e = comm_fetch(cm, st, &ok, flag.p, sizeof(ok), "root sampling")) return e;
         }
         if (!ok) continue;
         seen.insert(x);
@@ -1291,6 +1292,7 @@ int bfsx_level_stats(bfsx_graph *g, bfsx_level_stat *out, int cap) {
                 out[i].claims += o[i].claims;
                 out[i].stage2 += o[i].stage2;
                 out[i].walked += o[i].walked;
+                out[i].explicit_parents += o[i].explicit_parents;
                 out[i].kernel_ms = std::max(out[i].kernel_ms, o[i].kernel_ms);
                 out[i].cum_ms = std::max(out[i].cum_ms, o[i].cum_ms);
             }

@@ -471,6 +471,7 @@ void apply_options(Comm *c, const bfsx_ctx *ctx) {
 
 Comm::~Comm() {
     if (pinned) (void)hipHostFree(pinned);
+    for (void *p : pinned_retired) (void)hipHostFree(p);
 }
 
 int comm_fetch(Comm *cm, hipStream_t st, void *dst, const void *d_src, size_t bytes, const char *what) {
@@ -480,8 +481,9 @@ int comm_fetch(Comm *cm, hipStream_t st, void *dst, const void *d_src, size_t by
         return BFSX_OK;
     }
     if (bytes > cm->pinned_bytes) {
-        // the stream may still run a collective: the old buffer is no copy's target (every fetch drains its copy)
-        if (cm->pinned) (void)hipHostFree(cm->pinned);
+        // the stream may still run a collective, and hipHostFree would wait for it outside comm_sync's polling
+        // (a failed peer would then hang this rank): the old buffer is retired, freed with the communicator
+        if (cm->pinned) cm->pinned_retired.push_back(cm->pinned);
         cm->pinned = nullptr;
         cm->pinned_bytes = 0;
         const size_t cap = std::max<size_t>(bytes, 4096);

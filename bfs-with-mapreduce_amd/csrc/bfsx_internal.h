@@ -93,6 +93,9 @@ struct Comm {
     bool agreed = false;         // the error being returned was reached by every rank at the same point: no abort
     void *pinned = nullptr;      // comm_fetch's bounce buffer (page-locked host memory)
     size_t pinned_bytes = 0;
+    // bounce buffers replaced by a larger fetch: freed with the communicator, never while a collective may still
+    // be queued on the stream (hipHostFree waits for the device, outside the polled host waits)
+    std::vector<void *> pinned_retired;
     virtual ~Comm();
     virtual int allreduce_sum(int64_t *d_buf, int n, hipStream_t st) = 0;              // in place
     // one value per rank; d_recv[rank] (the value a rank sends itself) may be left unwritten

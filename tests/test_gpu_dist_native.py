@@ -505,6 +505,9 @@ def test_group_context_one_call(bfsx, world):
                 assert len(g.level_times()) == st["levels"] and len(g.level_dirs()) == st["levels"]
                 ls = g.level_stats()
                 assert sum(x["frontier_out"] for x in ls) == st["reached"] - 1
+                # a partition's pull levels store every parent explicitly, summed over the ranks like frontier_out
+                pulls = [x for x in ls if x["direction"] == 2]
+                assert sum(x["explicit_parents"] for x in pulls) == sum(x["frontier_out"] for x in pulls)
                 d2, p2 = g.result()
                 assert np.array_equal(d2, d) and np.array_equal(p2, p)
                 goff, gcol = g.csr()
@@ -599,3 +602,34 @@ def test_native_group_empty_push_workgroup_race(bfsx, world):
     errs = run_group_errors(bfsx, world, make, 0, {"race_probe": "nobarrier"})
     assert all(e is not None and "device guard" in e for e in errs), errs
     assert any("store guard" in e for e in errs), errs
+
+
+def test_group_context_rccl_clique():
+    """bfsx_init_group on distinct devices: an RCCL clique (ncclCommInitAll, threaded warm-up, the heap abort board).
+    It needs one device per rank, so it skips on a one-GPU box and runs by itself on a multi-GPU one
+    (BFSX_GROUP_COMM=rccl makes a group with fewer devices than ranks an error instead of an in-process group)."""
+    code = f"""
+import ctypes as C, sys, os, numpy as np
+n = C.c_int(0)
+C.CDLL("libamdhip64.so").hipGetDeviceCount(C.byref(n))
+if n.value < 2:
+    print("skip: %d device(s)" % n.value); sys.exit(0)
+sys.path.insert(0, {os.path.join(ROOT, 'tests')!r})
+import conftest, oracle_py as O
+bfsx = conftest.load_bfsx()
+P = min(n.value, 4)
+with bfsx.Context(group=P) as gc, bfsx.Context(0) as one:
+    with gc.kronecker(16, 16, 0x51) as g, one.kronecker(16, 16, 0x51) as g1:
+        for r in g.sample_roots(4).tolist():
+            d, p, st = g.bfs(r)
+            d1, _, st1 = g1.bfs(r)
+            assert np.array_equal(d, d1) and st["m_comp"] == st1["m_comp"]
+            assert g.validate()["errors"] == 0
+print("clique-ok", P)
+"""
+    env = dict(os.environ, BFSX_GROUP_COMM="rccl")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    if r.stdout.startswith("skip"):
+        pytest.skip(r.stdout.strip())
+    assert "clique-ok" in r.stdout, r.stdout + r.stderr
