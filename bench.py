@@ -108,6 +108,13 @@ def parse_args():
     ap.add_argument("--levels-json", default="")
     ap.add_argument("--option", action="append", default=[], help="libbfsx option key=value")
     ap.add_argument("--dist", action="store_true", help="use the partitioned path even on one rank (rehearsal)")
+    ap.add_argument("--scale30-roots", type=int, default=-1,
+                    help="N > 1: after the scale-26 metric, BASELINE configs[4] (RMAT scale 30, 1-D partitioned over the "
+                         "same ranks) on this many validated roots, reported as the line's 'scale30' object (-1: 4 "
+                         "roots when N > 1 and --scale is 26; 0: off)")
+    ap.add_argument("--comm-split-roots", type=int, default=8,
+                    help="N > 1: roots of the untimed diagnostic pass with hipEvents around every collective "
+                         "(per-kind device time per BFS, max over ranks; 0: off)")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank (and the --gpus N launcher) gives up and exits 124 instead of "
                          "waiting on a stuck peer (0: none)")
@@ -525,6 +532,119 @@ def run_single(args):
     print(json.dumps(out), flush=True)
 
 
+def rccl_debug_env(rank):
+    """Ask RCCL to log its connection setup (NCCL_DEBUG=INFO, INIT/P2P/NET subsystems) into a per-rank file, so
+    that rank 0 can report which transport its peers were connected over; left alone when the caller set
+    NCCL_DEBUG itself.  Must run before the first RCCL call."""
+    if os.environ.get("NCCL_DEBUG"):
+        return None
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"bfsx_rccl_{os.getpid()}_rank{rank}.log")
+    os.environ.update({"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,P2P,NET,GRAPH", "NCCL_DEBUG_FILE": path})
+    return path
+
+
+def rccl_transports(path):
+    """Transport summary of one rank's RCCL log: how many channel connections went over each transport
+    ("via P2P/IPC", "via NET/Socket/0", "via SHM/direct/direct", ...) and the communicator sizes RCCL reported."""
+    import re
+    if not path or not os.path.exists(path):
+        return {"note": "NCCL_DEBUG set by the caller: no transport log"}
+    via, nranks = {}, set()
+    with open(path, errors="replace") as f:
+        for ln in f:
+            m = re.search(r" via ([A-Za-z0-9_]+(?:/[A-Za-z0-9_]+)?)", ln)
+            if m:
+                via[m.group(1)] = via.get(m.group(1), 0) + 1
+            m = re.search(r"nRanks (\d+)", ln)
+            if m:
+                nranks.add(int(m.group(1)))
+    try:
+        os.unlink(path)
+    except OSError:
+        pass
+    return {"connections_by_transport": via, "comm_sizes_reported": sorted(nranks),
+            "note": "rank 0's RCCL INFO log (INIT/P2P/NET): P2P = GPU peer access over xGMI, SHM = host shared "
+                    "memory, NET = network (the one-GPU socket rehearsal)"}
+
+
+def comm_split(args, g, dist, torch, roots, world):
+    """Untimed diagnostic pass (option comm_timing): device time of every collective kind per BFS, and of every
+    level, each the max over the ranks -- where the time of an N > 1 BFS goes."""
+    n = min(args.comm_split_roots, len(roots))
+    if n <= 0:
+        return None
+    g.ctx.set_option("comm_timing", "on")
+    kinds = g.COMM_KINDS
+    acc, levels = np.zeros(2 * len(kinds)), None
+    try:
+        for r in roots[:n]:
+            g.dist_bfs(r, want_stats=False)
+            ct = g.comm_times()
+            t = torch.tensor([ct[k][0] for k in kinds] + [float(ct[k][1]) for k in kinds], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            acc += t.numpy()
+        ls = g.level_stats(256)
+        lt = torch.tensor([x["kernel_ms"] for x in ls], dtype=torch.float64)
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        levels = [{"level": x["level"], "direction": x["direction"], "ms_max_over_ranks": round(float(v), 4)}
+                  for x, v in zip(ls, lt.tolist())]
+    finally:
+        g.ctx.set_option("comm_timing", "off")
+    return {"roots": n,
+            "ms_per_bfs": {k: round(acc[i] / n, 4) for i, k in enumerate(kinds)},
+            "calls_per_bfs": {k: round(acc[len(kinds) + i] / n, 2) for i, k in enumerate(kinds)},
+            "levels_last_bfs": levels,
+            "note": "hipEvents around every collective of the level loop on the BFS stream (a span includes the wait "
+                    "for the slowest rank), summed per BFS, max over ranks, mean over the roots; levels: device "
+                    "time of each level of the last root, max over ranks"}
+
+
+def scale30_leg(args, bfsx, ctx, dist, torch, rank, world, shared_device):
+    """BASELINE configs[4]: RMAT scale 30, edgefactor 16, 1-D partitioned over the same ranks and communicator,
+    after the scale-26 metric: the first args.scale30_roots validated roots, one timed BFS each (device time, max
+    over ranks).  Every rank takes part; a rank that cannot build its slice makes every rank skip the leg."""
+    t0 = time.perf_counter()
+    g, err = None, ""
+    try:
+        if shared_device:
+            for r in range(world):
+                if r == rank:
+                    g = ctx.dist_kronecker(30, rank, world, args.edgefactor, args.seed)
+                    ctx.synchronize()
+                dist.barrier()
+        else:
+            g = ctx.dist_kronecker(30, rank, world, args.edgefactor, args.seed)
+            ctx.synchronize()
+    except bfsx.BfsxError as e:
+        err = str(e)
+    ok = torch.tensor([0 if err else 1], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok) == 0:
+        if g is not None:
+            g.free()
+        return {"error": f"build failed on some rank (this rank: {err or 'ok'})"}
+    build_s = time.perf_counter() - t0
+    sub = argparse.Namespace(**dict(vars(args), roots=args.scale30_roots))
+    roots, mcomp, val_errors, skipped = pick_roots(sub, g, g.m, lambda r: g.dist_bfs(r)["m_comp"],
+                                                   lambda: g.validate()["errors"])
+    ctx.synchronize()
+    dist.barrier()
+    ts = [g.dist_bfs(r, want_stats=False) for r in roots]
+    tt = torch.tensor(ts, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    split = comm_split(argparse.Namespace(comm_split_roots=min(2, len(roots))), g, dist, torch, roots, world)
+    part, m_tuples = g.partition(), g.m
+    g.free()
+    return {"metric": f"GTEPS (harmonic mean, {len(roots)} roots) on RMAT scale-30", "workload": "kronecker-s30-ef16",
+            "value": hmean([mcomp[r] / (t * 1e-3) / 1e9 for r, t in zip(roots, tt.tolist())]), "unit": "GTEPS",
+            "n_gpus": world, "nv": part["nv_global"], "m_tuples": m_tuples,
+            "t_bfs_ms_mean": float(np.mean(tt.tolist())), "graph_build_s": round(build_s, 3),
+            "validation": {"roots": len(roots), "errors": val_errors, "skipped_tiny_component": skipped},
+            "comm_split": split,
+            "note": "BASELINE configs[4]: one timed BFS per validated root after the scale-26 metric, device time "
+                    "(max over ranks), the same partitioned level loop and RCCL communicator"}
+
+
 def run_dist(args, world, rank, local_rank):
     """One process per GPU: the partitioned level loop and its RCCL exchange run inside libbfsx
     (bfsx_dist_bfs); torch.distributed (gloo, host only) is used for the rendezvous -- the RCCL unique
@@ -540,6 +660,7 @@ def run_dist(args, world, rank, local_rank):
         # (loopback). Never set by the driver's runs; see DESIGN §7.
         os.environ["NCCL_HOSTID"] = f"bfsx-rehearsal-rank{rank}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    rccl_log = rccl_debug_env(rank) if world > 1 else None
     # Gloo and RCCL print banners on the process's C-level stdout; the contract is ONE JSON line, so
     # fd 1 points at stderr until the result is printed
     sys.stdout.flush()
@@ -623,10 +744,24 @@ def run_dist(args, world, rank, local_rank):
                                    "rules": "Graph500 kernel-2 + BreadthFirstPaths.check, on device, collective"},
                     "levels_last": [{k: ls[k] for k in ("level", "direction", "frontier_in", "frontier_out",
                                                         "kernel_ms")} for ls in g.level_stats(256)]})
+    split = comm_split(args, g, dist, torch, roots, world) if world > 1 else None
+    if rank == 0:
+        out["comm_split"] = split
+        out["rccl"] = dict(world_size=world, devices_visible=ndev, device_of_rank0=device,
+                           shared_device_rehearsal=shared_device, **rccl_transports(rccl_log))
     if rank == 0 and args.levels_json:
         with open(args.levels_json, "w") as f:
             json.dump(all_levels, f)
     g.free()
+    s30 = args.scale30_roots if args.scale30_roots >= 0 else (4 if world > 1 and args.scale == 26 else 0)
+    if s30 > 0:
+        args.scale30_roots = s30
+        try:
+            leg = scale30_leg(args, bfsx, ctx, dist, torch, rank, world, shared_device)
+        except (bfsx.BfsxError, AssertionError) as e:
+            leg = {"error": str(e)}
+        if rank == 0:
+            out["scale30"] = leg
     ctx.close()
     dist.destroy_process_group()
     sys.stdout.flush()

@@ -43,6 +43,7 @@ EXPORTS = [
     "bfsx_dist_graph_from_edges", "bfsx_dist_graph_kronecker", "bfsx_graph_partition", "bfsx_graph_degree",
     "bfsx_last_bfs_ms", "bfsx_last_unpack_ms", "bfsx_persist_fallbacks", "bfsx_comm_unique_id", "bfsx_comm_init", "bfsx_comm_local_group",
     "bfsx_dist_bfs", "bfsx_init_group", "bfsx_group_size", "bfsx_dist_graph_load_algs4", "bfsx_last_resolve_ms",
+    "bfsx_comm_times",
 ]
 # test-only level primitives (include/bfsx_levels.h): exported for tests/dist_driver.py, not product ABI
 TEST_EXPORTS = [
@@ -129,6 +130,8 @@ def _bind(L):
         if hasattr(L, "bfsx_persist_fallbacks") or not os.environ.get("BFSX_LIB"):  # an older build (A/B) may lack it
             L.bfsx_persist_fallbacks.argtypes = [_VP, C.POINTER(C.c_int64)]
         L.bfsx_level_stats.argtypes = [_VP, C.POINTER(LevelStat), C.c_int]
+        if hasattr(L, "bfsx_comm_times") or not os.environ.get("BFSX_LIB"):  # an older build (A/B) may lack it
+            L.bfsx_comm_times.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         L.bfsx_device_synchronize.argtypes = [_VP]
         I64P = C.POINTER(C.c_int64)
         L.bfsx_validate.argtypes = [_VP, C.c_int64, I64P, I64P, I64P, I64P]
@@ -357,6 +360,15 @@ class Graph:
         ms = C.c_double()
         self._check(self._L.bfsx_last_bfs_ms(self._h, C.byref(ms)))
         return ms.value
+
+    COMM_KINDS = ("allreduce", "count_alltoall", "alltoallv", "allgather")
+
+    def comm_times(self):
+        """Device time (ms) and calls of the collectives of the most recent partitioned BFS by kind
+        (bfsx_comm_times; option comm_timing=on, else zeros): {"allreduce": (ms, calls), ...}."""
+        ms, cnt = (C.c_double * 4)(), (C.c_int64 * 4)()
+        self._check(self._L.bfsx_comm_times(self._h, ms, cnt))
+        return {k: (ms[i], cnt[i]) for i, k in enumerate(self.COMM_KINDS)}
 
     def last_unpack_ms(self):
         """Device time (ms) of the unpack kernel of the most recent result copy (bfsx_last_unpack_ms): the

@@ -243,6 +243,13 @@ struct BfsWorkspace {
         size_t bytes;
     };
     std::vector<Retired> retired;
+    // option comm_timing: event pairs around the level loop's collectives of the last partitioned BFS, their kind
+    // (CommOp - 1) and the per-kind sums bfsx_comm_times reads
+    std::vector<hipEvent_t> ev_comm;
+    std::vector<int> comm_kind;
+    int n_comm = 0;
+    double comm_ms[4] = {0, 0, 0, 0};
+    int64_t comm_n[4] = {0, 0, 0, 0};
 };
 
 // Debug aid (environment BFSX_SYNC_LAUNCH=1): synchronise the stream after every launch, so an asynchronous

@@ -563,6 +563,12 @@ static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
         ctx->opt.fail_level = (int)lv;
         return BFSX_OK;
     }
+    if (k == "comm_timing") {
+        if (v == "on") ctx->opt.comm_timing = true;
+        else if (v == "off") ctx->opt.comm_timing = false;
+        else return fail(BFSX_E_ARG, "comm_timing must be on|off");
+        return BFSX_OK;
+    }
     if (k == "race_probe") { // test hook
         if (v == "off") ctx->opt.race_probe = 0;
         else if (v == "delay") ctx->opt.race_probe = 1;
@@ -1243,6 +1249,28 @@ int bfsx_last_bfs_ms(const bfsx_graph *g, double *ms) {
 int bfsx_persist_fallbacks(const bfsx_graph *g, int64_t *count) {
     if (!g || !count) return fail(BFSX_E_ARG, "bad argument");
     *count = bfs_persist_fallbacks(g);
+    return BFSX_OK;
+}
+
+int bfsx_comm_times(const bfsx_graph *g, double *ms, int64_t *count) {
+    if (!g || !ms || !count) return fail(BFSX_E_ARG, "bad argument");
+    if (is_group(g)) { // the largest span over the ranks, per kind
+        for (int k = 0; k < 4; k++) {
+            ms[k] = 0.0;
+            count[k] = 0;
+        }
+        for (const bfsx_graph *p : g->parts) {
+            double m[4];
+            int64_t c[4];
+            bfs_comm_times(p, m, c);
+            for (int k = 0; k < 4; k++) {
+                ms[k] = std::max(ms[k], m[k]);
+                count[k] = std::max(count[k], c[k]);
+            }
+        }
+        return BFSX_OK;
+    }
+    bfs_comm_times(g, ms, count);
     return BFSX_OK;
 }
 

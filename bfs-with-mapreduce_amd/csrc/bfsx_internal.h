@@ -69,6 +69,7 @@ struct Options {
     int64_t comm_timeout_ms = 120000; // partitioned path: a host wait on the peers fails after this long
     bool check_collectives = false;   // debug: every collective checks that all ranks are in the same (op, level)
     int fail_rank = -1, fail_level = -1; // test hook (fault injection): that rank fails at that level of the loop
+    bool comm_timing = false;   // partitioned: hipEvents around every collective of the level loop (bfsx_comm_times)
     int race_probe = 0;         // test hook: k_td's queue init late behind stale LDS (1), and without its barrier (2)
     int64_t slot_force = -1;    // test hook: fixed-slot push levels use slots of this many pairs (the store guard fires)
 };
@@ -168,6 +169,7 @@ double bfs_last_unpack_ms(const bfsx_graph *g);
 // its first part: the push log scattered and the pull records folded into the per-vertex state (the result in
 // internal ids); -1 when the last copy took the scatter path (graphs without the relabel)
 double bfs_last_resolve_ms(const bfsx_graph *g);
+void bfs_comm_times(const bfsx_graph *g, double *ms, int64_t *count); // option comm_timing: last partitioned BFS
 // multi-GPU level primitives (kernels_dist.hip), driven by bfsx_dist_* in bfsx_api.cpp
 int dist_begin(bfsx_graph *g, int64_t source, int64_t *deg_local, int64_t deg_known = -1);
 int dist_frontier_info(bfsx_graph *g, int64_t *nf_local, int64_t *mf_local, int *in_queue);

@@ -479,6 +479,18 @@ int dist_finish(bfsx_graph *g) {
         BFSX_HIP_TRY(hipEventElapsedTime(&ms, ws->ev_start, ws->ev_end));
         g->last_t_bfs_ms = ms;
     }
+    for (int k = 0; k < 4; k++) {
+        ws->comm_ms[k] = 0.0;
+        ws->comm_n[k] = 0;
+    }
+    for (int i = 0; i < ws->n_comm; i++) { // option comm_timing (CommSpan): every span has completed by ev_end
+        float ms = 0.f;
+        const int k = ws->comm_kind[i];
+        if (k >= 0 && k < 4 && hipEventElapsedTime(&ms, ws->ev_comm[2 * i], ws->ev_comm[2 * i + 1]) == hipSuccess) {
+            ws->comm_ms[k] += ms;
+            ws->comm_n[k]++;
+        }
+    }
     const int levels = ws->d_level;
     g->level_cum_ms.resize(levels);
     for (int l = 0; l < levels; l++) {
@@ -524,6 +536,31 @@ void trace_buffers(const bfsx_graph *g, const BfsWorkspace *ws, int level) {
         fprintf(stderr, "[bfsx] rank %d level %d buffer %-8s [0x%llx, 0x%llx)\n", g->rank, level, x.name,
                 (unsigned long long)(uintptr_t)x.p, (unsigned long long)((uintptr_t)x.p + x.bytes));
 }
+
+// Option comm_timing: an event pair around one collective of the level loop on the BFS stream (bfsx_comm_times).
+// The end event is recorded when the scope ends, also on an early error return.
+struct CommSpan {
+    bfsx_graph *g;
+    BfsWorkspace *ws;
+    int idx = -1;
+    CommSpan(bfsx_graph *g_, BfsWorkspace *ws_, int op) : g(g_), ws(ws_) {
+        if (!g->ctx->opt.comm_timing) return;
+        const int k = ws->n_comm;
+        while ((int)ws->ev_comm.size() < 2 * (k + 1)) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            ws->ev_comm.push_back(e);
+        }
+        if ((int)ws->comm_kind.size() <= k) ws->comm_kind.resize(k + 1);
+        ws->comm_kind[k] = op - 1;
+        if (hipEventRecord(ws->ev_comm[2 * k], g->ctx->stream) != hipSuccess) return;
+        idx = k;
+        ws->n_comm = k + 1;
+    }
+    ~CommSpan() {
+        if (idx >= 0) (void)hipEventRecord(ws->ev_comm[2 * idx + 1], g->ctx->stream);
+    }
+};
 
 int grow(BfsWorkspace *ws, u64 *&buf, int64_t &cap, int64_t need) {
     if (need <= cap) return BFSX_OK;
@@ -636,7 +673,10 @@ int dist_level_close(bfsx_graph *g, BfsWorkspace *ws, bool td, int64_t out[kCtrS
     }
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     Comm *cm = g->ctx->comm.get();
-    if (int e = cm->allreduce_sum(sums + 8, 4 + g->nranks, st)) return e;
+    {
+        CommSpan span(g, ws, kOpAllreduce);
+        if (int e = cm->allreduce_sum(sums + 8, 4 + g->nranks, st)) return e;
+    }
     return post_wait(ws, st, reinterpret_cast<const u64 *>(sums), 12 + g->nranks, nullptr, 0,
                      reinterpret_cast<u64 *>(out), cm, "a level close");
 }
@@ -731,6 +771,7 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
     int64_t nf_core = -1;         // after a pull level: its local discoveries below leaf_lo (-1: unknown)
     ExchangePlan plan;
     std::vector<u64> hc(2 * kMaxRanks);
+    ws->n_comm = 0; // comm_timing: this BFS's collectives
     for (;;) {
         const int level = ws->d_level;
         cm->tag = level;
@@ -840,8 +881,11 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                                    (u64)ws->send_cap, ws->d_err);
                 BFSX_LAUNCHED(st);
                 u64 *drecv = ws->d_dist_ctr + kCtrRecv;
-                if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
-                    return e;
+                {
+                    CommSpan span(g, ws, kOpAlltoall1);
+                    if (int e = cm->alltoall1(reinterpret_cast<int64_t *>(dcount), reinterpret_cast<int64_t *>(drecv), st))
+                        return e;
+                }
                 if (int e = post_wait(ws, st, dcount, P, drecv, P, hc.data(), cm, "a pair-count exchange")) return e;
                 hc[P + g->rank] = 0; // alltoall1 does not exchange the own entry (no pairs route to it)
                 plan_counted(P, hc.data(), hc.data() + P, plan);
@@ -851,9 +895,12 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
             if (int e = check_live(g, ws, level, "pair exchange + claim",
                                    {{"sendbuf", ws->sendbuf}, {"recvbuf", ws->recvbuf}, {"remote", ws->remote}}))
                 return e;
-            if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
-                                      plan.rcount.data(), plan.rdispl.data(), st))
-                return e;
+            {
+                CommSpan span(g, ws, kOpAlltoallv);
+                if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
+                                          plan.rcount.data(), plan.rdispl.data(), st))
+                    return e;
+            }
             if (ro > 0) { // its last workgroup closes the level (the sums k_level_sums would compute)
                 const dim3 grid(clamp_grid((ro + kBS - 1) / kBS, cap));
                 const u64 qcap = (u64)std::max<int64_t>(plog ? g->nv - ws->log_n : g->nv, 0); // as the push kernels'
@@ -901,9 +948,12 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                                    {{"sendbuf", ws->sendbuf}, {"recvbuf", ws->recvbuf}, {"fglob", ws->fglob},
                                     {"record", rec}, {"vis", ws->vis}, {"parents", ws->par}}))
                 return e;
-            if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
-                                      plan.rcount.data(), plan.rdispl.data(), st))
-                return e;
+            {
+                CommSpan span(g, ws, kOpAlltoallv);
+                if (int e = cm->alltoallv(ws->sendbuf, plan.scount.data(), plan.sdispl.data(), ws->recvbuf,
+                                          plan.rcount.data(), plan.rdispl.data(), st))
+                    return e;
+            }
             BFSX_HIP_TRY(hipMemsetAsync(ws->fglob, 0, (size_t)ws->nwords * P * sizeof(u64), st));
             if (plan.recv_total > 0) {
                 hipLaunchKernelGGL(k_ids_to_bitmap, dim3(clamp_grid((plan.recv_total + kBS - 1) / kBS, cap)), dim3(kBS),
@@ -935,7 +985,10 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                                    {{"front", bmf}, {"fglob", ws->fglob}, {"record", rec}, {"vis", ws->vis},
                                     {"parents", ws->par}}))
                 return e;
-            if (int e = cm->allgather(bmf, ws->nwords, ws->fglob, st)) return e;
+            {
+                CommSpan span(g, ws, kOpAllgather);
+                if (int e = cm->allgather(bmf, ws->nwords, ws->fglob, st)) return e;
+            }
             if (int e = launch_bu<false>(g, ws, ws->fglob, rec, ws->par, level)) return e; // m_f from m_u (below)
             recs.done(level + 1);
             bmf = rec;

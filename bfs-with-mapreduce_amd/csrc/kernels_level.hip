@@ -630,6 +630,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     if (ws->ev_end) (void)hipEventDestroy(ws->ev_end);
     for (auto e : ws->ev_level) (void)hipEventDestroy(e);
     for (auto e : ws->ev_begin) (void)hipEventDestroy(e);
+    for (auto e : ws->ev_comm) (void)hipEventDestroy(e);
     delete ws;
 }
 
@@ -1267,5 +1268,11 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
 
 double bfs_last_unpack_ms(const bfsx_graph *g) { return g->ws ? g->ws->last_unpack_ms : -1.0; }
 double bfs_last_resolve_ms(const bfsx_graph *g) { return g->ws ? g->ws->last_resolve_ms : -1.0; }
+void bfs_comm_times(const bfsx_graph *g, double *ms, int64_t *count) {
+    for (int k = 0; k < 4; k++) {
+        ms[k] = g->ws ? g->ws->comm_ms[k] : 0.0;
+        count[k] = g->ws ? g->ws->comm_n[k] : 0;
+    }
+}
 
 } // namespace bfsx

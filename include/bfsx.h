@@ -29,8 +29,9 @@ extern "C" {
 #endif
 
 /* 2 (round 5): bfsx_level_stat gained explicit_parents at its end; bfsx_init_group, bfsx_group_size,
- * bfsx_dist_graph_load_algs4 and bfsx_last_resolve_ms were added */
-#define BFSX_ABI_VERSION 2
+ * bfsx_dist_graph_load_algs4 and bfsx_last_resolve_ms were added
+ * 3 (round 6): bfsx_comm_times was added (no layout changed) */
+#define BFSX_ABI_VERSION 3
 
 /* Error codes.  Mapping to the reference's exceptions:
  *   E_IO    <- IOException from FileInputStream / Files.write  (GraphFileUtil.java:43,46,68)
@@ -174,6 +175,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *                 collective of the same level, and fails on every rank with both names otherwise)
  *   "fail_at" = rank:level|rank:setup|off (test hook: that rank of a partitioned BFS fails at the start of that
  *                 level, or before its first collective)
+ *   "comm_timing" = on|off (partitioned graphs: hipEvents around every collective of the level loop, read by
+ *                 bfsx_comm_times; default off)
  *   "slot_force" = int|off (test hook: the fixed-slot push levels of a partitioned BFS use slots of this many
  *                 pairs, whatever the level's bound; a too-small slot makes the store guard fail the BFS on
  *                 every rank instead of writing past the slot)
@@ -311,6 +314,12 @@ int bfsx_comm_unique_id(uint8_t *id);
 int bfsx_comm_init(bfsx_ctx *ctx, int rank, int nranks, const uint8_t *id);
 int bfsx_comm_local_group(bfsx_ctx **ctxs, int nranks);
 int bfsx_dist_bfs(bfsx_graph *g, int64_t source, bfsx_stats *stats);
+/* Device time of the collectives of the most recent bfsx_dist_bfs on this rank, by kind, with option
+ * "comm_timing" on (default off: all zero): ms[0] the level-close all-reduces, ms[1] the pair-count
+ * all-to-alls, ms[2] the pair / frontier-id all-to-allvs, ms[3] the frontier all-gathers; count[k] the calls.
+ * A collective's span runs from the BFS stream reaching it to its completion, so it includes the wait for the
+ * slowest rank.  A group graph reports the largest span over its ranks per kind. */
+int bfsx_comm_times(const bfsx_graph *g, double *ms, int64_t *count);
 
 /* ---- device synchronisation helper for benchmarking harnesses ------------------------------- */
 int bfsx_device_synchronize(bfsx_ctx *ctx);

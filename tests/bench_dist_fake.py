@@ -17,7 +17,10 @@ def fake_bfsx():
         pass
 
     class Graph:
-        def __init__(self, scale, rank, world):
+        COMM_KINDS = ("allreduce", "count_alltoall", "alltoallv", "allgather")
+
+        def __init__(self, scale, rank, world, ctx=None):
+            self.ctx = ctx
             self.rank, self.world, self.nvg = rank, world, 1 << scale
             self.chunk = self.nvg // world
             self.nnz, self.m = 1000 + rank, 16 << scale
@@ -36,6 +39,13 @@ def fake_bfsx():
                 import time
                 time.sleep(3600)
             return 1.0 + 0.5 * self.rank + 0.01 * r  # device ms of this rank; rank world-1 is the slowest
+
+        def comm_times(self):
+            # per kind (ms, calls) of the last BFS: rank-dependent, so the line must carry the max over ranks;
+            # zeros unless the bench turned comm_timing on
+            on = self.ctx is not None and self.ctx.opts.get("comm_timing") == "on"
+            return {k: ((0.1 * (i + 1) + 0.01 * self.rank) if on else 0.0, (3 + self.rank) if on else 0)
+                    for i, k in enumerate(self.COMM_KINDS)}
 
         def validate(self, source=-1):
             return {"errors": 0}
@@ -59,15 +69,16 @@ def fake_bfsx():
     class Context:
         def __init__(self, device=0, **options):
             self.device = device
+            self.opts = dict(options)
 
         def set_option(self, k, v):
-            pass
+            self.opts[k] = v
 
         def comm_init(self, rank, world, uid):
             assert len(uid) == 128
 
         def dist_kronecker(self, scale, rank, world, edgefactor=16, seed=0):
-            return Graph(scale, rank, world)
+            return Graph(scale, rank, world, self)
 
         def synchronize(self):
             pass
@@ -91,7 +102,7 @@ def main():
     spec.loader.exec_module(bench)
     bench.load_module = lambda name, file: fake_bfsx()
     sys.argv = ["bench.py", "--gpus", os.environ["WORLD_SIZE"], "--scale", "12", "--roots", "4", "--steps", "2",
-                "--warmup", "1"]
+                "--warmup", "1"] + os.environ.get("BFSX_FAKE_EXTRA_ARGS", "").split()
     bench.main()
 
 

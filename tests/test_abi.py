@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     assert sorted(bfsx.EXPORTS) == declared_functions(HEADER)
     assert sorted(bfsx.TEST_EXPORTS) == declared_functions(LEVELS_HEADER)
     assert not set(bfsx.EXPORTS) & set(bfsx.TEST_EXPORTS)
-    assert L.bfsx_abi_version() == 2
+    assert L.bfsx_abi_version() == 3
 
 
 @pytest.mark.parametrize("so", ["libbfsx.so", "libbfsx_diag.so"])

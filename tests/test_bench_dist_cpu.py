@@ -94,3 +94,34 @@ def test_bench_shared_device_rehearsal_mode():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["bfs_runs"] == 8
+
+
+def test_bench_dist_line_diagnostics_and_scale30_leg():
+    """Round 6 (verdict item 5): the N > 1 line says where the time goes and covers configs[4].
+      comm_split  per collective kind, the device time per BFS (each BFS's max over ranks, mean over the roots) and
+                  the calls; the last root's per-level time, max over ranks
+      rccl        the world size and the transport summary of rank 0's RCCL log (no log here: a stand-in binding)
+      scale30     the scale-30 leg on the same ranks (--scale30-roots; on by default at N > 1 with --scale 26)"""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", BFSX_FAKE_EXTRA_ARGS="--scale30-roots 2",
+               NCCL_DEBUG="WARN")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "tests", "bench_dist_fake.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    cs = d["comm_split"]
+    assert cs["roots"] == 4  # min(--comm-split-roots 8, the 4 roots)
+    for i, k in enumerate(("allreduce", "count_alltoall", "alltoallv", "allgather")):
+        assert abs(cs["ms_per_bfs"][k] - (0.1 * (i + 1) + 0.01)) < 1e-9  # rank 1's, the slower
+        assert cs["calls_per_bfs"][k] == 4
+    assert [x["direction"] for x in cs["levels_last_bfs"]] == [1, 2]
+    assert d["rccl"]["world_size"] == 2 and "note" in d["rccl"]
+    s30 = d["scale30"]
+    assert s30["workload"] == "kronecker-s30-ef16" and s30["n_gpus"] == 2
+    assert s30["metric"] == "GTEPS (harmonic mean, 2 roots) on RMAT scale-30"
+    assert s30["validation"]["errors"] == 0 and s30["value"] > 0 and s30["comm_split"]["roots"] == 2

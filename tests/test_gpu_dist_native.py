@@ -633,3 +633,23 @@ print("clique-ok", P)
     if r.stdout.startswith("skip"):
         pytest.skip(r.stdout.strip())
     assert "clique-ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_native_group_comm_timing(bfsx):
+    """Option comm_timing: hipEvents around every collective of the level loop.  One level-close all-reduce per
+    level, one all-gather or id all-to-allv per pull level, one pair all-to-allv per push level that shipped; off
+    (the default) reports zeros.  A group graph reports the largest span over its ranks."""
+    scale, seed = 14, 0x77
+    with bfsx.Context(group=2, **GROUP_DEFAULTS) as gc, gc.kronecker(scale, 16, seed) as g:
+        r = int(g.sample_roots(1)[0])
+        g.bfs(r)
+        assert all(v == (0.0, 0) for v in g.comm_times().values())
+        gc.set_option("comm_timing", "on")
+        _, _, st = g.bfs(r)
+        ct = g.comm_times()
+        dirs = list(g.level_dirs())
+        assert ct["allreduce"][1] == st["levels"] and ct["allreduce"][0] > 0
+        pulls = sum(1 for x in dirs if x == 2)
+        assert ct["allgather"][1] + ct["alltoallv"][1] >= pulls
+        assert ct["alltoallv"][1] <= len(dirs) and all(ms >= 0 for ms, _ in ct.values())
+        gc.set_option("comm_timing", "off")
