@@ -534,9 +534,10 @@ def run_single(args):
 
 def rccl_debug_env(rank):
     """Ask RCCL to log its connection setup (NCCL_DEBUG=INFO, INIT/P2P/NET subsystems) into a per-rank file, so
-    that rank 0 can report which transport its peers were connected over; left alone when the caller set
-    NCCL_DEBUG itself.  Must run before the first RCCL call."""
-    if os.environ.get("NCCL_DEBUG"):
+    that rank 0 can report which transport its peers were connected over (its warnings are echoed to stderr
+    afterwards); left alone when the caller already directs RCCL's log to a file (NCCL_DEBUG_FILE) or asked for
+    more than INFO.  Must run before the first RCCL call."""
+    if os.environ.get("NCCL_DEBUG_FILE") or os.environ.get("NCCL_DEBUG", "").upper() in ("INFO", "TRACE"):
         return None
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"bfsx_rccl_{os.getpid()}_rank{rank}.log")
     os.environ.update({"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,P2P,NET,GRAPH", "NCCL_DEBUG_FILE": path})
@@ -548,10 +549,12 @@ def rccl_transports(path):
     ("via P2P/IPC", "via NET/Socket/0", "via SHM/direct/direct", ...) and the communicator sizes RCCL reported."""
     import re
     if not path or not os.path.exists(path):
-        return {"note": "NCCL_DEBUG set by the caller: no transport log"}
+        return {"note": "RCCL's log directed by the caller (NCCL_DEBUG_FILE / NCCL_DEBUG=INFO|TRACE): no transport summary"}
     via, nranks = {}, set()
     with open(path, errors="replace") as f:
         for ln in f:
+            if " WARN " in ln:
+                print(ln.rstrip(), file=sys.stderr)
             m = re.search(r" via ([A-Za-z0-9_]+(?:/[A-Za-z0-9_]+)?)", ln)
             if m:
                 via[m.group(1)] = via.get(m.group(1), 0) + 1
@@ -749,6 +752,8 @@ def run_dist(args, world, rank, local_rank):
         out["comm_split"] = split
         out["rccl"] = dict(world_size=world, devices_visible=ndev, device_of_rank0=device,
                            shared_device_rehearsal=shared_device, **rccl_transports(rccl_log))
+    elif rccl_log and os.path.exists(rccl_log):
+        os.unlink(rccl_log)
     if rank == 0 and args.levels_json:
         with open(args.levels_json, "w") as f:
             json.dump(all_levels, f)
