@@ -94,9 +94,10 @@ __global__ __launch_bounds__(kBS) void k_unpack_live(RecSet rs, int64_t live_n, 
         for (int j = 0; j < kUnpackU; j++) {
             const int64_t v = t0 + j * kBS + threadIdx.x;
             const bool live = v < live_n;
-            code[j] = (live && hit[j] >= 0) ? ps.code[v] : 0xFFu;
-            o1[j] = (live && hit[j] >= 0 && otop1) ? otop1[v] : 0u;
-            s[j] = (live && hit[j] < 0) ? stt[v] : kUnreached;
+            // streamed once (non-temporal: keep the Infinity Cache for tmp, which k_unpack_gather reads next)
+            code[j] = (live && hit[j] >= 0) ? __builtin_nontemporal_load(ps.code + v) : 0xFFu;
+            o1[j] = (live && hit[j] >= 0 && otop1) ? __builtin_nontemporal_load(otop1 + v) : 0u;
+            s[j] = (live && hit[j] < 0) ? __builtin_nontemporal_load(stt + v) : kUnreached;
         }
         // stage 2: the parent of every other kind -- an original id already (codes 0-3 with the copies), or an
         // internal id that goes through inv (explicit parents, st's)
@@ -152,11 +153,13 @@ __global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ t
     const int64_t lo = (int64_t)(blockIdx.x % kXcds) * per_xcd, hi = std::min<int64_t>(lo + per_xcd, n);
     const int64_t step = (int64_t)(gridDim.x / kXcds) * kTile;
     for (int64_t t0 = lo + (int64_t)(blockIdx.x / kXcds) * kTile; t0 < hi; t0 += step) {
+        // perm and out are streamed once (non-temporal: they should not push tmp, which k_unpack_live just wrote,
+        // out of the Infinity Cache); tmp is gathered
         int64_t i[kUnpackU];
 #pragma unroll
         for (int j = 0; j < kUnpackU; j++) {
             const int64_t o = t0 + j * kBS + threadIdx.x;
-            i[j] = o < hi ? (int64_t)perm[o] : iso_lo;
+            i[j] = o < hi ? (int64_t)__builtin_nontemporal_load(perm + o) : iso_lo;
         }
         u64 s[kUnpackU];
 #pragma unroll
@@ -165,8 +168,8 @@ __global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ t
         for (int j = 0; j < kUnpackU; j++) {
             const int64_t o = t0 + j * kBS + threadIdx.x;
             if (o >= hi) continue;
-            if (dist_only) dist_only[o] = (int32_t)(uint32_t)s[j];
-            else out[o] = s[j];
+            if (dist_only) __builtin_nontemporal_store((int32_t)(uint32_t)s[j], dist_only + o);
+            else __builtin_nontemporal_store(s[j], out + o);
         }
     }
 }
