@@ -102,7 +102,9 @@ struct alignas(128) PersistCtl {
 };
 // host-visible result of one launch (mapped pinned memory, written by workgroup 0)
 struct alignas(64) PersistOut {
-    u64 levels, abort, t0, done, pad[4]; // done: set by workgroup 0 once levels / abort / the records are final
+    u64 levels, abort, t0, done; // done: set by workgroup 0 once levels / abort / the records are final
+    u64 front;                   // the launch stopped for Beamer's rule and left its last frontier as a bitmap too
+    u64 pad[3];
     PersistRec rec[kPersistLevels];
 };
 
@@ -766,7 +768,7 @@ int ensure_heavy_rows(bfsx_graph *g, BfsWorkspace *ws);
 int persist_blocks(const bfsx_ctx *ctx);
 int persist_setup(bfsx_graph *g, BfsWorkspace *ws);
 bool persist_fits(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t dmax, bool heavy_src = false);
-int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu, uint32_t h0_v = 0,
+int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu, u64 *front, uint32_t h0_v = 0,
                uint32_t h0_deg = 0, int64_t h0_beg = 0);
 constexpr int kPersistAborted = -1000; // internal: K3p aborted (barrier timeout); bfs_run retries without it
 // kernels_dist.hip
@@ -823,12 +825,15 @@ namespace {
 
 // ---- K2: BFS init: visited bitmap <- dead mask (+ the source bit), source state, counter slots ------
 // s: local row of the source (0xFFFFFFFF: the source is owned by another rank); sglob: its global id.
+// front != null: also zero the frontier bitmap a BFS's first K3p launch may hand its last frontier back in
 __global__ __launch_bounds__(kBS) void k_init(uint32_t s, uint32_t sglob, int64_t prev, const u64 *__restrict__ dead,
                                               int64_t nwords, u64 *stt, u64 *__restrict__ vis, uint32_t *q,
-                                              LevelSlot *ring) {
+                                              LevelSlot *ring, u64 *__restrict__ front = nullptr) {
     const int64_t sw = s != 0xFFFFFFFFu ? (int64_t)(s >> 6) : -1;
-    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
         vis[w] = dead[w] | (w == sw ? 1ull << (s & 63u) : 0ull);
+        if (front) front[w] = 0ull;
+    }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         // a previous isolated source is pre-visited (dead mask) so k_finalize never resets it
         if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) stt[prev] = kUnreached;

@@ -700,7 +700,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // ---- timed region: source init -> last level ----
     if (record_start) BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
-                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring);
+                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring,
+                       (opt.persist && opt.persist_front && opt.direction == BFSX_DIR_AUTO) ? ws->front : nullptr);
     BFSX_LAUNCHED(st);
     ws->prev_source = source;
 
@@ -722,6 +723,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     int64_t nh_found = -1;
     // the last (sparse) pull level already wrote the next push level's queue into ws->qa (nf_core ids)
     bool queue_ready = false;
+    // the last K3p launch stopped for a pull level and also left its frontier in ws->front (option persist_front)
+    bool front_ready = false;
     int td_levels = 0, bu_levels = 0;
     // the bitmap frontier: ws->front after a push -> pull conversion, a pull level's record after a pull level
     const u64 *bmf = ws->front;
@@ -816,7 +819,10 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             if (nf == 0) break;
             continue;
         }
-        if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
+        if (dir == BFSX_DIR_BOTTOMUP && in_queue && front_ready) {
+            bmf = ws->front; // K3p stopped for this pull level and left the frontier in front as well
+            in_queue = false;
+        } else if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
             if (snapped) { // front holds the visited bitmap from before the last top-down level
                 hipLaunchKernelGGL(k_new_bits, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
                                    ws->vis, nwords, ws->front);
@@ -862,13 +868,17 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         nh_found = -1;
         queue_ready = false;
         snapped = false;
+        front_ready = false;
         u64 *plog = nullptr; // this level's push-log segment (a per-level push level with push_log)
         // level 0: a source row longer than persist_dmax enters K3p as its heavy table (row bounds known)
         const bool heavy_src = level == 0 && nf == 1 && dmax > opt.persist_dmax;
         if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax, heavy_src)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
-            const int ran = heavy_src ? persist_td(g, ws, level, 0, mu, (uint32_t)source, (uint32_t)dmax, src_off[0])
-                                      : persist_td(g, ws, level, nf, mu);
+            // the BFS's first launch hands a frontier that Beamer sends to a pull level back as the bitmap too
+            u64 *kfront = (level == 0 && opt.direction == BFSX_DIR_AUTO && opt.persist_front) ? ws->front : nullptr;
+            const int ran = heavy_src ? persist_td(g, ws, level, 0, mu, kfront, (uint32_t)source, (uint32_t)dmax,
+                                                   src_off[0])
+                                      : persist_td(g, ws, level, nf, mu, kfront);
             if (ran < 0) return ran;
             // ran == 0: K3p unavailable on this device (occupancy check): per-level launches below
             if (ran > 0) {
@@ -898,6 +908,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                     mfh = has_hubs(ws) ? (int64_t)r.mfh : -1;
                 }
                 std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
+                front_ready = po.front != 0;
                 td_levels += ran;
                 level += ran - 1;
                 if (nf == 0) break;

@@ -159,7 +159,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                     int alpha, int max_levels, u64 bar0, PersistCtl *ctl,
                                                     PersistOut *out, HubSet hs, int64_t bu_floor,
                                                     int inject_abort, u64 heavy_deg, uint32_t nrows, u64 *err,
-                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg) {
+                                                    u64 *hseg, uint32_t h0_v, uint32_t h0_deg, int64_t h0_beg,
+                                                    u64 *front, int64_t front_words) {
     extern __shared__ char s_dyn[]; // sized by the host so that one workgroup fills a CU's LDS share
     __shared__ uint32_t s_off[kBS + 1];
     __shared__ uint32_t s_hoff[kBS + 1];
@@ -182,6 +183,10 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         for (int i = tid; i < 3 * kSlotWords; i += kBS) p[i] = 0ull;
         if (tid == 0) out->t0 = (u64)wall_clock64();
     }
+    // front != null (a BFS's first launch): should the launch stop because Beamer asks for a pull level, its last
+    // frontier is also handed back as the `front` bitmap the pull kernel reads (no memset + queue -> bitmap pass
+    // between the launch and the pull).  k_init zeroed it (a kernel boundary before this launch).
+    (void)front_words;
     uint32_t nf = nf0, nh_in = h0_deg ? 1u : 0u;
     u64 eh_in = h0_deg;
     int64_t mu = mu0;
@@ -496,19 +501,31 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         // (Beamer's m_f > m_u / alpha as a product: the same decision as the host's for m_u >= 0, without a
         // 64-bit division on every workgroup's critical path)
         const bool beamer = alpha > 0 && (mu >= 0 ? (int64_t)mf_new * alpha > mu : (int64_t)mf_new > mu / alpha);
+        const bool to_pull = nf_all > 0 && beamer && (int64_t)mf_new > bu_floor; // the host's switch, the same test
         const bool stop = nf_all == 0 || nf_new > kPersistNf || nh_new > kHeavyMax ||
                           (u64)((nf_new + G - 1) / G) * dm_new + (kHeavy ? (eh_new + G - 1) / G : 0ull) > (u64)kRegion ||
-                          (beamer && (int64_t)mf_new > bu_floor) ||
-                          it + 1 >= max_levels;
+                          to_pull || it + 1 >= max_levels;
         __syncthreads();
         // the host reads the counts as soon as they are final (a mapped flag, no stream synchronise: that cost ~13 us
         // per launch); the hand-back below is stream-ordered before the next kernel anyway
-        if (stop && b == 0 && tid == 0) persist_done(out);
-        if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones
+        const bool bits = front && to_pull;
+        if (stop && b == 0 && tid == 0) {
+            out->front = bits ? 1ull : 0ull;
+            persist_done(out);
+        }
+        if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones (+ the bitmap)
             const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
-            for (uint32_t i = tid; i < nb; i += kBS) qfinal[ob + i] = (uint32_t)ld_sc1(sout + 2 * i + 1);
+            for (uint32_t i = tid; i < nb; i += kBS) {
+                const uint32_t v = (uint32_t)ld_sc1(sout + 2 * i + 1);
+                qfinal[ob + i] = v;
+                if (bits) atomicOr(front + (v >> 6), 1ull << (v & 63u));
+            }
             const uint32_t hb = (b + 1 < G ? s_hoff[b + 1] : nh_new) - s_hoff[b], hbase = nf_new + s_hoff[b];
-            for (uint32_t i = tid; i < hb; i += kBS) qfinal[hbase + i] = (uint32_t)ld_sc1(hout + 2 * i + 1);
+            for (uint32_t i = tid; i < hb; i += kBS) {
+                const uint32_t v = (uint32_t)ld_sc1(hout + 2 * i + 1);
+                qfinal[hbase + i] = v;
+                if (bits) atomicOr(front + (v >> 6), 1ull << (v & 63u));
+            }
             return;
         }
         nf = nf_new;
@@ -629,7 +646,7 @@ bool persist_fits(bfsx_graph *g, BfsWorkspace *ws, int64_t nf, int64_t dmax, boo
 // Run K3p from `level` (frontier of nf vertices in ws->qa; its last frontier lands in ws->qb).
 // Returns the number of levels it ran (>= 1) with their records in the PersistOut, or an error.
 // h0_deg > 0: the first level's frontier is the single heavy row {h0_v, h0_beg, h0_deg} (nf = 0 light).
-int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu, uint32_t h0_v,
+int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t mu, u64 *front, uint32_t h0_v,
                uint32_t h0_deg, int64_t h0_beg) {
     hipStream_t st = g->ctx->stream;
     const Options &opt = g->ctx->opt;
@@ -646,6 +663,7 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
     out->levels = 0;
     out->abort = 0;
     out->done = 0;
+    out->front = 0;
     std::atomic_thread_fence(std::memory_order_release);
     const int alpha = opt.direction == BFSX_DIR_AUTO ? std::max(opt.alpha, 1) : 0;
     auto *ctl = reinterpret_cast<PersistCtl *>(ws->persist_ctl);
@@ -662,13 +680,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, front, ws->nwords);
     else
         hipLaunchKernelGGL(kp64, grid, dim3(kBS), lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, front, ws->nwords);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     // spin on workgroup 0's flag; poll the stream now and then so a faulted launch surfaces as an error

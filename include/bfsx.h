@@ -116,6 +116,8 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
  *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS)
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
+ *   "persist_front" = on|off (a BFS's first such launch that stops because the next level pulls also leaves its
+ *                 last frontier as the pull kernel's bitmap, saving the queue -> bitmap pass; default on)
  *   "push_log" = on|off (one device: a per-level push level writes its winners as (vertex, parent) pairs at
  *                 their queue positions instead of scattered state stores; the result read scatters them;
  *                 default on)
