@@ -825,15 +825,12 @@ namespace {
 
 // ---- K2: BFS init: visited bitmap <- dead mask (+ the source bit), source state, counter slots ------
 // s: local row of the source (0xFFFFFFFF: the source is owned by another rank); sglob: its global id.
-// front != null: also zero the frontier bitmap a BFS's first K3p launch may hand its last frontier back in
 __global__ __launch_bounds__(kBS) void k_init(uint32_t s, uint32_t sglob, int64_t prev, const u64 *__restrict__ dead,
                                               int64_t nwords, u64 *stt, u64 *__restrict__ vis, uint32_t *q,
-                                              LevelSlot *ring, u64 *__restrict__ front = nullptr) {
+                                              LevelSlot *ring) {
     const int64_t sw = s != 0xFFFFFFFFu ? (int64_t)(s >> 6) : -1;
-    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS) {
+    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
         vis[w] = dead[w] | (w == sw ? 1ull << (s & 63u) : 0ull);
-        if (front) front[w] = 0ull;
-    }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         // a previous isolated source is pre-visited (dead mask) so k_finalize never resets it
         if (prev >= 0 && ((dead[prev >> 6] >> (prev & 63)) & 1ull)) stt[prev] = kUnreached;

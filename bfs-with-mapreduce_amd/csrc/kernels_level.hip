@@ -700,14 +700,12 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     // ---- timed region: source init -> last level ----
     if (record_start) BFSX_HIP_TRY(hipEventRecord(ws->ev_start, st));
     hipLaunchKernelGGL(k_init, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, (uint32_t)source,
-                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring,
-                       (opt.persist && opt.persist_front && opt.direction == BFSX_DIR_AUTO) ? ws->front : nullptr);
+                       (uint32_t)source, ws->prev_source, ws->dead, nwords, ws->st, ws->vis, ws->qa, ws->ring);
     BFSX_LAUNCHED(st);
     ws->prev_source = source;
 
     int dir = (opt.direction == BFSX_DIR_BOTTOMUP) ? BFSX_DIR_BOTTOMUP : BFSX_DIR_TOPDOWN;
     bool in_queue = true; // frontier currently held in ws->qa (else in ws->front)
-    bool snapped = false; // ws->front holds the visited bitmap from before the last (top-down) level
     int64_t nf = 1, prev_nf = 0;
     int64_t mf = src_off[1] - src_off[0]; // degree sum of the frontier being expanded (-1: unknown)
     int64_t dmax = mf;                    // its largest degree (-1: unknown)
@@ -767,10 +765,9 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             hybrid = opt.hybrid == 2 || 100 * mfh > (int64_t)opt.hybrid_pct * unv;
         }
         if (hybrid) {
-            BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
-            hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st, ws->qa,
-                               (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
-            BFSX_LAUNCHED(st);
+            // the hub sweep's frontier: a copy of the visited bitmap (every visited vertex a candidate can touch is
+            // in the frontier: see the pull levels below)
+            BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
             u64 *rec = nullptr;
             if (int e = recs.take(&rec)) return e;
             if (int e = launch_bu_hubonly(g, ws, ws->front, rec, ws->par, level)) return e; // -> rec, vis, par
@@ -812,7 +809,6 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             nh_found = -1;
             queue_ready = false;
             in_queue = false;
-            snapped = false;
             bu_levels++;
             recs.done(level + 1);
             bmf = rec;
@@ -823,15 +819,13 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             bmf = ws->front; // K3p stopped for this pull level and left the frontier in front as well
             in_queue = false;
         } else if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
-            if (snapped) { // front holds the visited bitmap from before the last top-down level
-                hipLaunchKernelGGL(k_new_bits, dim3(clamp_grid((nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                                   ws->vis, nwords, ws->front);
-            } else {
-                BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, nwords * sizeof(u64), st));
-                hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((nf + kBS - 1) / kBS, cap)), dim3(kBS), 0, st,
-                                   ws->qa, (uint32_t)nf, ws->front, (uint32_t)g->nv, ws->d_err);
-            }
-            BFSX_LAUNCHED(st);
+            // The pull level's frontier bitmap after a push level: a copy of the visited bitmap, not the frontier
+            // alone.  Level-synchronous BFS: before level L every vertex at distance <= L is visited, and an
+            // unvisited vertex has no neighbour at distance < L (it would have been discovered), so the only
+            // visited vertices its probes can meet ARE the frontier -- the same hits in the same row order, the
+            // same parents and distances -- for one 8-B copy per 64 ids instead of an atomic per frontier vertex
+            // (round 6; rounds 1-5 snapshotted the bitmap before a wide push level and XOR-ed it after).
+            BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
             bmf = ws->front;
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue && queue_ready) {
@@ -867,7 +861,6 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         nf_core = -1;
         nh_found = -1;
         queue_ready = false;
-        snapped = false;
         front_ready = false;
         u64 *plog = nullptr; // this level's push-log segment (a per-level push level with push_log)
         // level 0: a source row longer than persist_dmax enters K3p as its heavy table (row bounds known)
@@ -916,12 +909,6 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             }
         }
         if (dir == BFSX_DIR_TOPDOWN) {
-            // a wide top-down level may hand over to bottom-up: snapshot the visited bitmap (8 B per 64
-            // vertices) so its frontier bitmap is one XOR pass instead of one atomic per discovered vertex
-            if (mf >= nwords / 4 && opt.direction == BFSX_DIR_AUTO) {
-                BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
-                snapped = true;
-            }
             const Part pt = single_part(g, ws);
             // test hook: the level's kernels read one entry past the queue's tail (the guard must catch it)
             const int64_t nf_l = (BFSX_DIAG_ON && level == opt.test_overread) ? nf + 1 : nf;

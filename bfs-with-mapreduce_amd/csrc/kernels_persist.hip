@@ -183,10 +183,11 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         for (int i = tid; i < 3 * kSlotWords; i += kBS) p[i] = 0ull;
         if (tid == 0) out->t0 = (u64)wall_clock64();
     }
-    // front != null (a BFS's first launch): should the launch stop because Beamer asks for a pull level, its last
-    // frontier is also handed back as the `front` bitmap the pull kernel reads (no memset + queue -> bitmap pass
-    // between the launch and the pull).  k_init zeroed it (a kernel boundary before this launch).
-    (void)front_words;
+    // front != null (a BFS's first launch): should the launch stop because Beamer asks for a pull level, it also
+    // leaves the pull kernel's frontier bitmap in `front`: a copy of the visited bitmap.  A pull level may take
+    // every visited vertex as frontier: an unvisited vertex has no neighbour at a distance below the level's (it
+    // would have been discovered), so its probes meet exactly the frontier's bits either way, in the same row order
+    // -- the same parents, the same distances.  No memset, no queue -> bitmap atomics.
     uint32_t nf = nf0, nh_in = h0_deg ? 1u : 0u;
     u64 eh_in = h0_deg;
     int64_t mu = mu0;
@@ -514,17 +515,39 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
             persist_done(out);
         }
         if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones (+ the bitmap)
+            // 8 loads in flight per thread before their stores (a one-element loop waits a round trip per element)
+            constexpr int kCp = 8;
             const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
-            for (uint32_t i = tid; i < nb; i += kBS) {
-                const uint32_t v = (uint32_t)ld_sc1(sout + 2 * i + 1);
-                qfinal[ob + i] = v;
-                if (bits) atomicOr(front + (v >> 6), 1ull << (v & 63u));
+            for (uint32_t i0 = 0; i0 < nb; i0 += kBS * kCp) {
+                uint32_t e[kCp];
+#pragma unroll
+                for (int k = 0; k < kCp; k++) {
+                    const uint32_t i = i0 + (uint32_t)k * kBS + tid;
+                    e[k] = i < nb ? (uint32_t)ld_sc1(sout + 2 * i + 1) : 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < kCp; k++) {
+                    const uint32_t i = i0 + (uint32_t)k * kBS + tid;
+                    if (i < nb) qfinal[ob + i] = e[k];
+                }
             }
             const uint32_t hb = (b + 1 < G ? s_hoff[b + 1] : nh_new) - s_hoff[b], hbase = nf_new + s_hoff[b];
-            for (uint32_t i = tid; i < hb; i += kBS) {
-                const uint32_t v = (uint32_t)ld_sc1(hout + 2 * i + 1);
-                qfinal[hbase + i] = v;
-                if (bits) atomicOr(front + (v >> 6), 1ull << (v & 63u));
+            for (uint32_t i = tid; i < hb; i += kBS) qfinal[hbase + i] = (uint32_t)ld_sc1(hout + 2 * i + 1);
+            if (bits) { // every claim of the level completed before its record (vmcnt(0)); sc1 loads see them all
+                const int64_t w0 = front_words * b / G, w1 = front_words * (b + 1) / G;
+                for (int64_t x0 = w0; x0 < w1; x0 += (int64_t)kBS * kCp) {
+                    u64 e[kCp];
+#pragma unroll
+                    for (int k = 0; k < kCp; k++) {
+                        const int64_t w = x0 + (int64_t)k * kBS + tid;
+                        e[k] = w < w1 ? ld_sc1(vis + w) : 0ull;
+                    }
+#pragma unroll
+                    for (int k = 0; k < kCp; k++) {
+                        const int64_t w = x0 + (int64_t)k * kBS + tid;
+                        if (w < w1) front[w] = e[k];
+                    }
+                }
             }
             return;
         }
