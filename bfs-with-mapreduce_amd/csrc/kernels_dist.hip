@@ -761,7 +761,6 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
     // the next push level's pair buffers).
     int64_t mu_local = g->nnz - (owner ? deg_local : 0);
     int64_t visited_local = owner ? 1 : 0;
-    bool snapped = false; // ws->front holds the visited slice from before the last (top-down) level
     int td_levels = 0, bu_levels = 0;
     // the local bitmap frontier: ws->front after a push -> pull conversion, the last pull level's record after a
     // pull level; pull levels store 4-B parents plus their record, as on one device (RecLog, BfsWorkspace::par)
@@ -794,8 +793,6 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
         const bool td = dir == BFSX_DIR_TOPDOWN;
         bool summed = false; // the level's last kernel already closed the level (k_claim_remote)
         u64 *plog = nullptr; // a push level's push-log segment
-        const bool was_snapped = snapped;
-        snapped = false;
         int64_t nq = ws->d_nf; // the push queue's length
         if (td) {
             if (!ws->d_in_queue) { // local bitmap slice -> queue
@@ -814,12 +811,6 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
                 BFSX_LAUNCHED(st);
                 if (skip) nq = nf_core;
                 ws->d_in_queue = true;
-            }
-            // a wide top-down level may hand over to bottom-up: snapshot the visited slice (see bfs_run)
-            if (ws->d_mf >= ws->nwords / 4 && opt.direction == BFSX_DIR_AUTO) {
-                BFSX_HIP_TRY(
-                    hipMemcpyAsync(ws->front, ws->vis, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
-                snapped = true;
             }
             // remote pairs <= adjacency entries of the local frontier
             const int64_t need = std::max<int64_t>(ws->d_mf, 1);
@@ -966,16 +957,10 @@ int dist_bfs_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, Comm *cm) {
             bmf = rec;
             bu_levels++;
         } else {
-            if (ws->d_in_queue) { // local queue -> bitmap slice
-                if (was_snapped) { // front holds the visited slice from before the last top-down level
-                    hipLaunchKernelGGL(k_new_bits, dim3(clamp_grid((ws->nwords + kBS - 1) / kBS, cap)), dim3(kBS), 0,
-                                       st, ws->vis, ws->nwords, ws->front);
-                } else {
-                    BFSX_HIP_TRY(hipMemsetAsync(ws->front, 0, ws->nwords * sizeof(u64), st));
-                    hipLaunchKernelGGL(k_queue_to_bitmap, dim3(clamp_grid((ws->d_nf + kBS - 1) / kBS, cap)), dim3(kBS),
-                                       0, st, ws->qa, (uint32_t)ws->d_nf, ws->front, (uint32_t)g->nv, ws->d_err);
-                }
-                BFSX_LAUNCHED(st);
+            if (ws->d_in_queue) { // after a push level: the visited slice stands for the frontier slice
+                // (every visited vertex an unvisited one can touch is in the frontier: kernels_level.hip, bfs_run;
+                // globally the same, so the all-gathered visited slices serve the pull kernel as the frontier)
+                BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, ws->nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
                 bmf = ws->front;
                 ws->d_in_queue = false;
             }

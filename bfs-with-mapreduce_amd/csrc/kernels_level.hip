@@ -52,7 +52,10 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, Par
 // scale 26 in a rocprof trace, against ~0.15 ms each at the streaming rate).  So every thread handles kUnpackU
 // elements per step -- tiles of kBS * kUnpackU consecutive ids per workgroup, every load of a stage issued
 // before the first is used.
-constexpr int kUnpackU = 8;
+#ifndef BFSX_UNPACK_U
+#define BFSX_UNPACK_U 8
+#endif
+constexpr int kUnpackU = BFSX_UNPACK_U;
 
 // otop1[v] / orest[v]: top1 / rest with their entries mapped to original ids (built once per graph, at its first
 // unpack; the degree-1 flag of top1 dropped)
@@ -815,6 +818,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             if (nf == 0) break;
             continue;
         }
+        if (front_ready && dir != BFSX_DIR_BOTTOMUP) // K3p left no queue: its stop test is this switch's
+            return fail(BFSX_E_HIP, "internal error: the persistent launch stopped for a pull level the loop did not take");
         if (dir == BFSX_DIR_BOTTOMUP && in_queue && front_ready) {
             bmf = ws->front; // K3p stopped for this pull level and left the frontier in front as well
             in_queue = false;

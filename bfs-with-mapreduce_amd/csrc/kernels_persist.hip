@@ -517,7 +517,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         if (stop) { // hand the frontier back contiguous: the light entries, then the heavy ones (+ the bitmap)
             // 8 loads in flight per thread before their stores (a one-element loop waits a round trip per element)
             constexpr int kCp = 8;
-            const uint32_t nb = (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
+            // bits: the host's next level is the pull (the same test as to_pull), which reads `front`, not the queue
+            const uint32_t nb = bits ? 0u : (b + 1 < G ? s_off[b + 1] : nf_new) - s_off[b], ob = s_off[b];
             for (uint32_t i0 = 0; i0 < nb; i0 += kBS * kCp) {
                 uint32_t e[kCp];
 #pragma unroll
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                     if (i < nb) qfinal[ob + i] = e[k];
                 }
             }
-            const uint32_t hb = (b + 1 < G ? s_hoff[b + 1] : nh_new) - s_hoff[b], hbase = nf_new + s_hoff[b];
+            const uint32_t hb = bits ? 0u : (b + 1 < G ? s_hoff[b + 1] : nh_new) - s_hoff[b], hbase = nf_new + s_hoff[b];
             for (uint32_t i = tid; i < hb; i += kBS) qfinal[hbase + i] = (uint32_t)ld_sc1(hout + 2 * i + 1);
             if (bits) { // every claim of the level completed before its record (vmcnt(0)); sc1 loads see them all
                 const int64_t w0 = front_words * b / G, w1 = front_words * (b + 1) / G;
