@@ -51,7 +51,11 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, Par
 // iteration leaves them latency-bound (each wave waits a whole memory round trip per element: 0.35 + 0.30 ms at
 // scale 26 in a rocprof trace, against ~0.15 ms each at the streaming rate).  So every thread handles kUnpackU
 // elements per step -- tiles of kBS * kUnpackU consecutive ids per workgroup, every load of a stage issued
-// before the first is used.
+// before the first is used.  Round 6 found that the source did not get that from hipcc: a load under a per-id
+// condition became a branch followed by s_waitcnt vmcnt(0), so the stages still went one round trip per element.
+// The branch-free forms (k_unpack_live4, k_unpack_gather) issue every load and select afterwards: 0.47-0.48 ->
+// 0.37-0.39 ms per scale-26 result (profiles/r06ub_unpack_ab.txt).  k_unpack_live stays for a graph without the
+// codes or the original-id copies.
 #ifndef BFSX_UNPACK_U
 #define BFSX_UNPACK_U 8
 #endif
@@ -144,34 +148,198 @@ __global__ __launch_bounds__(kBS) void k_unpack_live(RecSet rs, int64_t live_n, 
     }
 }
 
+// 16-B non-temporal loads (the builtin takes clang vector types, not HIP's uint4)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load4(const void *p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// k_unpack_live, branch-free (round 6): four consecutive internal ids per lane, and no load behind a per-id
+// branch.  hipcc puts a branch around a conditional load and waits for every outstanding load after it
+// (s_waitcnt vmcnt(0)), so the per-id `cond ? load : default` of k_unpack_live issued its loads one round trip
+// at a time.  Here every load is issued, with the address of an element that needs none moved to entry 0 of its
+// array (a line every wave touches: no extra HBM traffic), and the value selected afterwards.  Four ids per lane
+// also make the streaming accesses wide: the codes of four ids are one 4-B load, their otop1 entries one 16-B
+// load, their states two 16-B loads and their tmp words two 16-B stores.  Needs the codes and otop1 / orest
+// (else k_unpack_live); a tile that crosses live_n takes k_unpack_live's per-id path.
+constexpr int kLiveRecUnroll = 4; // record words loaded together (a BFS has 2-4 pull levels; more loop)
+__global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n, int64_t src, ParSrc ps,
+                                                      const uint32_t *__restrict__ otop1,
+                                                      const uint4 *__restrict__ orest, const u64 *__restrict__ stt,
+                                                      const uint32_t *__restrict__ inv, u64 *__restrict__ tmp,
+                                                      int64_t n) {
+    constexpr int64_t kTile = (int64_t)kBS * 8;
+    for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < live_n; t0 += (int64_t)gridDim.x * kTile) {
+        if (t0 + kTile > live_n) { // the last tile: per id (uniform branch)
+            for (int64_t v = t0 + threadIdx.x; v < live_n; v += kBS) {
+                int hit = -1;
+                for (int r = 0; r < rs.n; r++)
+                    if ((rs.bm[r][v >> 6] >> (v & 63)) & 1ull) hit = r;
+                uint32_t p, d;
+                bool mapped = false;
+                if (hit < 0) {
+                    const u64 x = stt[v];
+                    p = (uint32_t)(x >> 32);
+                    d = (uint32_t)x;
+                } else {
+                    d = (uint32_t)rs.nd[hit];
+                    const uint32_t c = ps.code[v];
+                    if (c == kCodeTop1) {
+                        p = otop1[v];
+                        mapped = true;
+                    } else if (c < kCodeExplicit) {
+                        const uint4 r = orest[v];
+                        p = c == 1 ? r.x : c == 2 ? r.y : r.z;
+                        mapped = true;
+                    } else {
+                        p = ps.par[v];
+                    }
+                }
+                if (!mapped && p != 0xFFFFFFFFu) p = inv[p];
+                tmp[v] = ((u64)p << 32) | d;
+            }
+            continue;
+        }
+        int64_t v0[2];
+#pragma unroll
+        for (int g = 0; g < 2; g++) v0[g] = t0 + g * (kBS * 4) + threadIdx.x * 4;
+        // stage 0: the record words (16 lanes share one), the first kLiveRecUnroll records issued together
+        unsigned nib[2] = {0u, 0u}; // per group: ids found by some pull level
+        uint32_t hd[8];            // their distance (a record's level + 1; taken with the record's uniform index)
+#pragma unroll
+        for (int j = 0; j < 8; j++) hd[j] = 0u;
+        {
+            u64 w[kLiveRecUnroll][2];
+#pragma unroll
+            for (int r = 0; r < kLiveRecUnroll; r++)
+#pragma unroll
+                for (int g = 0; g < 2; g++) // past rs.n (maybe none: a BFS without pull levels) read st instead
+                    w[r][g] = (r < rs.n ? rs.bm[r] : stt)[v0[g] >> 6];
+#pragma unroll
+            for (int r = 0; r < kLiveRecUnroll; r++)
+#pragma unroll
+                for (int g = 0; g < 2; g++) {
+                    const unsigned m = r < rs.n ? (unsigned)(w[r][g] >> (v0[g] & 63)) & 0xFu : 0u;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if ((m >> k) & 1u) hd[g * 4 + k] = (uint32_t)rs.nd[r];
+                    nib[g] |= m;
+                }
+        }
+        for (int r = kLiveRecUnroll; r < rs.n; r++) // records are disjoint
+#pragma unroll
+            for (int g = 0; g < 2; g++) {
+                const unsigned m = (unsigned)(rs.bm[r][v0[g] >> 6] >> (v0[g] & 63)) & 0xFu;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if ((m >> k) & 1u) hd[g * 4 + k] = (uint32_t)rs.nd[r];
+                nib[g] |= m;
+            }
+        // stage 1: codes + otop1 of groups with a record vertex, states of groups with another one
+        uint32_t code4[2];
+        uint4 o1[2], sa[2], sb[2];
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            const int64_t vh = nib[g] ? v0[g] : 0, va = (~nib[g] & 3u) ? v0[g] : 0, vb = (~nib[g] & 12u) ? v0[g] : 0;
+            code4[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps.code + vh));
+            o1[g] = nt_load4(otop1 + vh);
+            sa[g] = nt_load4(stt + va);
+            sb[g] = nt_load4(stt + vb + 2);
+        }
+        // stage 2: orest for codes 1-3, the explicit parent for code 4
+        uint32_t p[8], d[8];
+        uint4 ro[8];
+        uint32_t pe[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int g = j >> 2, k = j & 3;
+            const uint32_t c = (code4[g] >> (8 * k)) & 0xFFu;
+            const bool rec = (nib[g] >> k) & 1u;
+            const int64_t v = v0[g] + k;
+            ro[j] = orest[(rec && c != kCodeTop1 && c < kCodeExplicit) ? v : 0];
+            pe[j] = ps.par[(rec && c >= kCodeExplicit) ? v : 0];
+        }
+        bool need_inv[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int g = j >> 2, k = j & 3;
+            const uint32_t c = (code4[g] >> (8 * k)) & 0xFFu;
+            const uint4 sv = k < 2 ? sa[g] : sb[g];
+            const uint32_t sp = (k & 1) ? sv.w : sv.y, sd = (k & 1) ? sv.z : sv.x;
+            const uint32_t ot = k == 0 ? o1[g].x : k == 1 ? o1[g].y : k == 2 ? o1[g].z : o1[g].w;
+            // masks, not a select chain: the chain became a dynamic component index into scratch
+            const uint32_t orr = (ro[j].x & (0u - (uint32_t)(c == 1))) | (ro[j].y & (0u - (uint32_t)(c == 2))) |
+                                 (ro[j].z & (0u - (uint32_t)(c == 3)));
+            if (!((nib[g] >> k) & 1u)) {
+                p[j] = sp;
+                d[j] = sd;
+                need_inv[j] = sp != 0xFFFFFFFFu;
+            } else {
+                d[j] = hd[j];
+                p[j] = c == kCodeTop1 ? ot : c < kCodeExplicit ? orr : pe[j];
+                need_inv[j] = c >= kCodeExplicit && pe[j] != 0xFFFFFFFFu;
+            }
+        }
+        // stage 3: internal parents -> original ids
+        uint32_t q[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) q[j] = inv[need_inv[j] ? p[j] : 0u];
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (need_inv[j]) p[j] = q[j];
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            u64 *t = tmp + v0[g];
+            *reinterpret_cast<uint4 *>(t) = make_uint4(d[g * 4], p[g * 4], d[g * 4 + 1], p[g * 4 + 1]);
+            *reinterpret_cast<uint4 *>(t + 2) = make_uint4(d[g * 4 + 2], p[g * 4 + 2], d[g * 4 + 3], p[g * 4 + 3]);
+        }
+    }
+    // an isolated source lies in the tail the loop skips: its state (distance 0, itself as parent) is in st
+    if (src >= live_n && src < n && blockIdx.x == 0 && threadIdx.x == 0) {
+        const u64 s = stt[src];
+        tmp[src] = ((u64)inv[(uint32_t)(s >> 32)] << 32) | (uint32_t)s;
+    }
+}
+
 // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8), each with its own L2, so the
 // grid is cut into 8 contiguous ranges of original ids, one per XCD.  A degree class whose members are sparse in
 // the original order then shares its tmp lines inside one L2 instead of every XCD fetching each line.
 constexpr int kXcds = 8;
+// Phase 2.  Branch-free (round 6, see k_unpack_live4): a whole tile's perm loads are issued together and every
+// tmp load is issued (an isolated id's at entry 0), then selected; the stores need no per-id test.  XCD ranges
+// are whole tiles, so only a tile that crosses its range's end takes the per-id path.
+template <bool kDistOnly>
 __global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ tmp, const uint32_t *__restrict__ perm,
-                                                       int64_t n, int64_t iso_lo, int64_t src, u64 *__restrict__ out,
-                                                       int32_t *__restrict__ dist_only) {
+                                                          int64_t n, int64_t iso_lo, int64_t src, u64 *__restrict__ out,
+                                                          int32_t *__restrict__ dist_only) {
     constexpr int64_t kTile = (int64_t)kBS * kUnpackU;
-    const int64_t per_xcd = (n + kXcds - 1) / kXcds;
+    const int64_t per_xcd = ((n + kXcds - 1) / kXcds + kTile - 1) / kTile * kTile;
     const int64_t lo = (int64_t)(blockIdx.x % kXcds) * per_xcd, hi = std::min<int64_t>(lo + per_xcd, n);
     const int64_t step = (int64_t)(gridDim.x / kXcds) * kTile;
     for (int64_t t0 = lo + (int64_t)(blockIdx.x / kXcds) * kTile; t0 < hi; t0 += step) {
-        // perm and out are streamed once (non-temporal: they should not push tmp, which k_unpack_live just wrote,
-        // out of the Infinity Cache); tmp is gathered
-        int64_t i[kUnpackU];
-#pragma unroll
-        for (int j = 0; j < kUnpackU; j++) {
-            const int64_t o = t0 + j * kBS + threadIdx.x;
-            i[j] = o < hi ? (int64_t)__builtin_nontemporal_load(perm + o) : iso_lo;
+        if (t0 + kTile > hi) { // per id
+            for (int64_t o = t0 + threadIdx.x; o < hi; o += kBS) {
+                const int64_t i = perm[o];
+                const u64 s = (i < iso_lo || i == src) ? tmp[i] : kUnreached;
+                if (kDistOnly) dist_only[o] = (int32_t)(uint32_t)s;
+                else out[o] = s;
+            }
+            continue;
         }
+        uint32_t i[kUnpackU];
+#pragma unroll
+        for (int j = 0; j < kUnpackU; j++) i[j] = __builtin_nontemporal_load(perm + t0 + j * kBS + threadIdx.x);
         u64 s[kUnpackU];
 #pragma unroll
-        for (int j = 0; j < kUnpackU; j++) s[j] = (i[j] < iso_lo || i[j] == src) ? tmp[i[j]] : kUnreached;
+        for (int j = 0; j < kUnpackU; j++) {
+            const bool live = (int64_t)i[j] < iso_lo || (int64_t)i[j] == src;
+            s[j] = tmp[live ? i[j] : 0u];
+            s[j] = live ? s[j] : kUnreached;
+        }
 #pragma unroll
         for (int j = 0; j < kUnpackU; j++) {
             const int64_t o = t0 + j * kBS + threadIdx.x;
-            if (o >= hi) continue;
-            if (dist_only) __builtin_nontemporal_store((int32_t)(uint32_t)s[j], dist_only + o);
+            if (kDistOnly) __builtin_nontemporal_store((int32_t)(uint32_t)s[j], dist_only + o);
             else __builtin_nontemporal_store(s[j], out + o);
         }
     }
@@ -1191,15 +1359,24 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         }
         const int64_t live_n = std::min<int64_t>(ws->iso_lo, (int64_t)nv);
         const int64_t tile = (int64_t)kBS * kUnpackU;
-        hipLaunchKernelGGL(k_unpack_live, dim3(clamp_grid((live_n + tile - 1) / tile, 4096)), dim3(kBS), 0, st,
-                           rs, live_n, src, par_src(ws), ws->otop1, ws->orest, ws->st, g->d_inv, tmp, (int64_t)nv);
+        if (ws->otop1 && ws->pcode) // the branch-free pass needs the codes and the original-id copies
+            hipLaunchKernelGGL(k_unpack_live4, dim3(clamp_grid((live_n + kBS * 8 - 1) / (kBS * 8), 4096)), dim3(kBS), 0,
+                               st, rs, live_n, src, par_src(ws), ws->otop1, ws->orest, ws->st, g->d_inv, tmp,
+                               (int64_t)nv);
+        else
+            hipLaunchKernelGGL(k_unpack_live, dim3(clamp_grid((live_n + tile - 1) / tile, 4096)), dim3(kBS), 0, st,
+                               rs, live_n, src, par_src(ws), ws->otop1, ws->orest, ws->st, g->d_inv, tmp, (int64_t)nv);
         BFSX_LAUNCHED(st);
         BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack_mid, st));
         // a multiple of the XCD count, about one tile per workgroup
         const unsigned gx = std::max<unsigned>(
             kXcds, clamp_grid(((int64_t)nv + (int64_t)kBS * kUnpackU - 1) / ((int64_t)kBS * kUnpackU), 4096) / kXcds * kXcds);
-        hipLaunchKernelGGL(k_unpack_gather, dim3(gx), dim3(kBS), 0, st, tmp, g->d_perm, (int64_t)nv, ws->iso_lo, src,
-                           ws->out64, d_dist_only);
+        if (d_dist_only)
+            hipLaunchKernelGGL(k_unpack_gather<true>, dim3(gx), dim3(kBS), 0, st, tmp, g->d_perm, (int64_t)nv,
+                               ws->iso_lo, src, ws->out64, d_dist_only);
+        else
+            hipLaunchKernelGGL(k_unpack_gather<false>, dim3(gx), dim3(kBS), 0, st, tmp, g->d_perm, (int64_t)nv,
+                               ws->iso_lo, src, ws->out64, d_dist_only);
         ws->out_mode = 0; // every entry written: a later scatter-mode unpack must prefill again
     } else if (g->d_inv)
         hipLaunchKernelGGL(k_unpack<true>, grid, dim3(kBS), 0, st, ws->st, par_src(ws), rs, g->d_inv, g->v_lo, (int64_t)nv,
