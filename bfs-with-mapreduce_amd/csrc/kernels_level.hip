@@ -54,12 +54,18 @@ __global__ __launch_bounds__(kBS) void k_unpack(const u64 *__restrict__ stt, Par
 // before the first is used.  Round 6 found that the source did not get that from hipcc: a load under a per-id
 // condition became a branch followed by s_waitcnt vmcnt(0), so the stages still went one round trip per element.
 // The branch-free forms (k_unpack_live4, k_unpack_gather) issue every load and select afterwards: 0.47-0.48 ->
-// 0.37-0.39 ms per scale-26 result (profiles/r06ub_unpack_ab.txt).  k_unpack_live stays for a graph without the
-// codes or the original-id copies.
+// 0.37-0.39 ms per scale-26 result (profiles/r06ub_unpack_ab.txt), 0.35 with 16 ids per thread in the gather.
+// k_unpack_live stays for a graph without the codes or the original-id copies.
 #ifndef BFSX_UNPACK_U
 #define BFSX_UNPACK_U 8
 #endif
 constexpr int kUnpackU = BFSX_UNPACK_U;
+// k_unpack_gather's ids per thread and tile step (16: 0.39 -> 0.35 ms per scale-26 result against 8; 24 equal, 32
+// and 4 slower: profiles/r06uu_gather_unroll_ab.txt, r06uv_gather_unroll_ab.txt)
+#ifndef BFSX_GATHER_U
+#define BFSX_GATHER_U 16
+#endif
+constexpr int kGatherU = BFSX_GATHER_U;
 
 // otop1[v] / orest[v]: top1 / rest with their entries mapped to original ids (built once per graph, at its first
 // unpack; the degree-1 flag of top1 dropped)
@@ -163,12 +169,17 @@ __device__ __forceinline__ uint4 nt_load4(const void *p) {
 // load, their states two 16-B loads and their tmp words two 16-B stores.  Needs the codes and otop1 / orest
 // (else k_unpack_live); a tile that crosses live_n takes k_unpack_live's per-id path.
 constexpr int kLiveRecUnroll = 4; // record words loaded together (a BFS has 2-4 pull levels; more loop)
+#ifndef BFSX_LIVE_G
+#define BFSX_LIVE_G 2
+#endif
+// groups of four consecutive ids per lane and tile (1-4 within 1%: profiles/r06lg_live_groups_ab.txt)
+constexpr int kLiveG = BFSX_LIVE_G;
 __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n, int64_t src, ParSrc ps,
                                                       const uint32_t *__restrict__ otop1,
                                                       const uint4 *__restrict__ orest, const u64 *__restrict__ stt,
                                                       const uint32_t *__restrict__ inv, u64 *__restrict__ tmp,
                                                       int64_t n) {
-    constexpr int64_t kTile = (int64_t)kBS * 8;
+    constexpr int64_t kTile = (int64_t)kBS * 4 * kLiveG;
     for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < live_n; t0 += (int64_t)gridDim.x * kTile) {
         if (t0 + kTile > live_n) { // the last tile: per id (uniform branch)
             for (int64_t v = t0 + threadIdx.x; v < live_n; v += kBS) {
@@ -200,25 +211,25 @@ __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n,
             }
             continue;
         }
-        int64_t v0[2];
+        int64_t v0[kLiveG];
 #pragma unroll
-        for (int g = 0; g < 2; g++) v0[g] = t0 + g * (kBS * 4) + threadIdx.x * 4;
+        for (int g = 0; g < kLiveG; g++) v0[g] = t0 + g * (kBS * 4) + threadIdx.x * 4;
         // stage 0: the record words (16 lanes share one), the first kLiveRecUnroll records issued together
-        unsigned nib[2] = {0u, 0u}; // per group: ids found by some pull level
-        uint32_t hd[8];            // their distance (a record's level + 1; taken with the record's uniform index)
+        unsigned nib[kLiveG] = {}; // per group: ids found by some pull level
+        uint32_t hd[4 * kLiveG];            // their distance (a record's level + 1; taken with the record's uniform index)
 #pragma unroll
-        for (int j = 0; j < 8; j++) hd[j] = 0u;
+        for (int j = 0; j < 4 * kLiveG; j++) hd[j] = 0u;
         {
-            u64 w[kLiveRecUnroll][2];
+            u64 w[kLiveRecUnroll][kLiveG];
 #pragma unroll
             for (int r = 0; r < kLiveRecUnroll; r++)
 #pragma unroll
-                for (int g = 0; g < 2; g++) // past rs.n (maybe none: a BFS without pull levels) read st instead
+                for (int g = 0; g < kLiveG; g++) // past rs.n (maybe none: a BFS without pull levels) read st instead
                     w[r][g] = (r < rs.n ? rs.bm[r] : stt)[v0[g] >> 6];
 #pragma unroll
             for (int r = 0; r < kLiveRecUnroll; r++)
 #pragma unroll
-                for (int g = 0; g < 2; g++) {
+                for (int g = 0; g < kLiveG; g++) {
                     const unsigned m = r < rs.n ? (unsigned)(w[r][g] >> (v0[g] & 63)) & 0xFu : 0u;
 #pragma unroll
                     for (int k = 0; k < 4; k++)
@@ -228,7 +239,7 @@ __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n,
         }
         for (int r = kLiveRecUnroll; r < rs.n; r++) // records are disjoint
 #pragma unroll
-            for (int g = 0; g < 2; g++) {
+            for (int g = 0; g < kLiveG; g++) {
                 const unsigned m = (unsigned)(rs.bm[r][v0[g] >> 6] >> (v0[g] & 63)) & 0xFu;
 #pragma unroll
                 for (int k = 0; k < 4; k++)
@@ -236,10 +247,10 @@ __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n,
                 nib[g] |= m;
             }
         // stage 1: codes + otop1 of groups with a record vertex, states of groups with another one
-        uint32_t code4[2];
-        uint4 o1[2], sa[2], sb[2];
+        uint32_t code4[kLiveG];
+        uint4 o1[kLiveG], sa[kLiveG], sb[kLiveG];
 #pragma unroll
-        for (int g = 0; g < 2; g++) {
+        for (int g = 0; g < kLiveG; g++) {
             const int64_t vh = nib[g] ? v0[g] : 0, va = (~nib[g] & 3u) ? v0[g] : 0, vb = (~nib[g] & 12u) ? v0[g] : 0;
             code4[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps.code + vh));
             o1[g] = nt_load4(otop1 + vh);
@@ -247,11 +258,11 @@ __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n,
             sb[g] = nt_load4(stt + vb + 2);
         }
         // stage 2: orest for codes 1-3, the explicit parent for code 4
-        uint32_t p[8], d[8];
-        uint4 ro[8];
-        uint32_t pe[8];
+        uint32_t p[4 * kLiveG], d[4 * kLiveG];
+        uint4 ro[4 * kLiveG];
+        uint32_t pe[4 * kLiveG];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < 4 * kLiveG; j++) {
             const int g = j >> 2, k = j & 3;
             const uint32_t c = (code4[g] >> (8 * k)) & 0xFFu;
             const bool rec = (nib[g] >> k) & 1u;
@@ -259,9 +270,9 @@ __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n,
             ro[j] = orest[(rec && c != kCodeTop1 && c < kCodeExplicit) ? v : 0];
             pe[j] = ps.par[(rec && c >= kCodeExplicit) ? v : 0];
         }
-        bool need_inv[8];
+        bool need_inv[4 * kLiveG];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < 4 * kLiveG; j++) {
             const int g = j >> 2, k = j & 3;
             const uint32_t c = (code4[g] >> (8 * k)) & 0xFFu;
             const uint4 sv = k < 2 ? sa[g] : sb[g];
@@ -281,14 +292,14 @@ __global__ __launch_bounds__(kBS) void k_unpack_live4(RecSet rs, int64_t live_n,
             }
         }
         // stage 3: internal parents -> original ids
-        uint32_t q[8];
+        uint32_t q[4 * kLiveG];
 #pragma unroll
-        for (int j = 0; j < 8; j++) q[j] = inv[need_inv[j] ? p[j] : 0u];
+        for (int j = 0; j < 4 * kLiveG; j++) q[j] = inv[need_inv[j] ? p[j] : 0u];
 #pragma unroll
-        for (int j = 0; j < 8; j++)
+        for (int j = 0; j < 4 * kLiveG; j++)
             if (need_inv[j]) p[j] = q[j];
 #pragma unroll
-        for (int g = 0; g < 2; g++) {
+        for (int g = 0; g < kLiveG; g++) {
             u64 *t = tmp + v0[g];
             *reinterpret_cast<uint4 *>(t) = make_uint4(d[g * 4], p[g * 4], d[g * 4 + 1], p[g * 4 + 1]);
             *reinterpret_cast<uint4 *>(t + 2) = make_uint4(d[g * 4 + 2], p[g * 4 + 2], d[g * 4 + 3], p[g * 4 + 3]);
@@ -312,7 +323,7 @@ template <bool kDistOnly>
 __global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ tmp, const uint32_t *__restrict__ perm,
                                                           int64_t n, int64_t iso_lo, int64_t src, u64 *__restrict__ out,
                                                           int32_t *__restrict__ dist_only) {
-    constexpr int64_t kTile = (int64_t)kBS * kUnpackU;
+    constexpr int64_t kTile = (int64_t)kBS * kGatherU;
     const int64_t per_xcd = ((n + kXcds - 1) / kXcds + kTile - 1) / kTile * kTile;
     const int64_t lo = (int64_t)(blockIdx.x % kXcds) * per_xcd, hi = std::min<int64_t>(lo + per_xcd, n);
     const int64_t step = (int64_t)(gridDim.x / kXcds) * kTile;
@@ -326,18 +337,18 @@ __global__ __launch_bounds__(kBS) void k_unpack_gather(const u64 *__restrict__ t
             }
             continue;
         }
-        uint32_t i[kUnpackU];
+        uint32_t i[kGatherU];
 #pragma unroll
-        for (int j = 0; j < kUnpackU; j++) i[j] = __builtin_nontemporal_load(perm + t0 + j * kBS + threadIdx.x);
-        u64 s[kUnpackU];
+        for (int j = 0; j < kGatherU; j++) i[j] = __builtin_nontemporal_load(perm + t0 + j * kBS + threadIdx.x);
+        u64 s[kGatherU];
 #pragma unroll
-        for (int j = 0; j < kUnpackU; j++) {
+        for (int j = 0; j < kGatherU; j++) {
             const bool live = (int64_t)i[j] < iso_lo || (int64_t)i[j] == src;
             s[j] = tmp[live ? i[j] : 0u];
             s[j] = live ? s[j] : kUnreached;
         }
 #pragma unroll
-        for (int j = 0; j < kUnpackU; j++) {
+        for (int j = 0; j < kGatherU; j++) {
             const int64_t o = t0 + j * kBS + threadIdx.x;
             if (kDistOnly) __builtin_nontemporal_store((int32_t)(uint32_t)s[j], dist_only + o);
             else __builtin_nontemporal_store(s[j], out + o);
@@ -1360,7 +1371,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         const int64_t live_n = std::min<int64_t>(ws->iso_lo, (int64_t)nv);
         const int64_t tile = (int64_t)kBS * kUnpackU;
         if (ws->otop1 && ws->pcode) // the branch-free pass needs the codes and the original-id copies
-            hipLaunchKernelGGL(k_unpack_live4, dim3(clamp_grid((live_n + kBS * 8 - 1) / (kBS * 8), 4096)), dim3(kBS), 0,
+            hipLaunchKernelGGL(k_unpack_live4, dim3(clamp_grid((live_n + kBS * 4 * kLiveG - 1) / (kBS * 4 * kLiveG), 4096)), dim3(kBS), 0,
                                st, rs, live_n, src, par_src(ws), ws->otop1, ws->orest, ws->st, g->d_inv, tmp,
                                (int64_t)nv);
         else
@@ -1370,7 +1381,7 @@ int bfs_copy_result(bfsx_graph *g, int32_t *dist_out, int64_t *parent_out) {
         BFSX_HIP_TRY(hipEventRecord(ws->ev_unpack_mid, st));
         // a multiple of the XCD count, about one tile per workgroup
         const unsigned gx = std::max<unsigned>(
-            kXcds, clamp_grid(((int64_t)nv + (int64_t)kBS * kUnpackU - 1) / ((int64_t)kBS * kUnpackU), 4096) / kXcds * kXcds);
+            kXcds, clamp_grid(((int64_t)nv + (int64_t)kBS * kGatherU - 1) / ((int64_t)kBS * kGatherU), 4096) / kXcds * kXcds);
         if (d_dist_only)
             hipLaunchKernelGGL(k_unpack_gather<true>, dim3(gx), dim3(kBS), 0, st, tmp, g->d_perm, (int64_t)nv,
                                ws->iso_lo, src, ws->out64, d_dist_only);
