@@ -24,8 +24,8 @@ timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 300 $B --levels-json "$OUT/levels.json" > "$OUT/bench_levels.json" 2> "$OUT/bench_levels.err"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $B \
     > "$OUT/trace.log" 2>&1
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_bu|k_finalize|k_td" --output-format csv \
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_bu|k_finalize|k_td|k_unpack|k_resolve_log" --output-format csv \
     -d "$OUT/pmc_fetch" -o run -- $B > "$OUT/pmc_fetch.log" 2>&1
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_bu|k_finalize|k_td" --output-format csv \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_bu|k_finalize|k_td|k_unpack|k_resolve_log" --output-format csv \
     -d "$OUT/pmc_write" -o run -- $B > "$OUT/pmc_write.log" 2>&1
 echo done > "$OUT/DONE"
