@@ -175,6 +175,21 @@ JNIEXPORT jbyteArray JNICALL Java_it_unitn_bd_bfs_Bfsx_commUniqueId(JNIEnv *env,
     return out;
 }
 
+JNIEXPORT void JNICALL Java_it_unitn_bd_bfs_Bfsx_commTimes(JNIEnv *env, jclass cls, jlong g, jdoubleArray ms,
+                                                          jlongArray calls) {
+    double m[4];
+    int64_t c[4];
+    if ((*env)->GetArrayLength(env, ms) < 4 || (*env)->GetArrayLength(env, calls) < 4) {
+        throw_for(env, BFSX_E_ARG);
+        return;
+    }
+    if (failed(env, bfsx_comm_times(H(g), m, c))) return;
+    jlong cl[4];
+    for (int k = 0; k < 4; k++) cl[k] = (jlong)c[k];
+    (*env)->SetDoubleArrayRegion(env, ms, 0, 4, m);
+    (*env)->SetLongArrayRegion(env, calls, 0, 4, cl);
+}
+
 JNIEXPORT void JNICALL Java_it_unitn_bd_bfs_Bfsx_commInit(JNIEnv *env, jclass cls, jlong ctx, jint rank, jint nranks,
                                                          jbyteArray id) {
     uint8_t buf[BFSX_COMM_ID_BYTES];

@@ -79,6 +79,13 @@ public final class Bfsx {
     /** 128 bytes: rank 0 creates them, a Spark Broadcast<byte[]> (or any channel) ships them. */
     public static native byte[] commUniqueId();
 
+    /**
+     * Device time (ms[4]) and calls (calls[4]) per collective kind of the last distributed BFS on this rank, with
+     * option "comm_timing" on: level-close all-reduces, pair-count all-to-alls, pair / id all-to-allvs, frontier
+     * all-gathers (bfsx_comm_times).  Take the max over ranks.
+     */
+    public static native void commTimes(long graph, double[] ms, long[] calls) throws IOException;
+
     public static native void commInit(long ctx, int rank, int nranks, byte[] id);
 
     public static native long distKronecker(long ctx, int scale, int edgefactor, long seed, int rank, int nranks);
