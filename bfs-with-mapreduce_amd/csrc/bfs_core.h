@@ -148,6 +148,10 @@ struct BfsWorkspace {
     int64_t log_meta_cap = 0;
     uint32_t *off32 = nullptr;          // uint32 copy of the row offsets (nnz < 2^32), else null
     u64 *vis = nullptr, *front = nullptr, *next = nullptr;
+    // single device (option vis_front): the second visited buffer.  A pull level whose frontier is the visited
+    // bitmap itself (after a push, hybrid or K3p level) reads vis and writes vis | its discoveries into
+    // bu_vis_out (= vis2, one-shot, consumed by the next pull launch); the loop then swaps vis and vis2
+    u64 *vis2 = nullptr, *bu_vis_out = nullptr;
     u64 *dead = nullptr;                // isolated vertices + padding (initial visited bitmap)
     int64_t n_dead = 0;                 // isolated vertices (excluding padding)
     uint32_t *top1 = nullptr;           // first (highest-degree) neighbour of every vertex (+ kDeg1 flag)

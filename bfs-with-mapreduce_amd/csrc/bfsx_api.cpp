@@ -438,6 +438,12 @@ static int set_option_one(bfsx_ctx *ctx, const char *key, const char *value) {
         else return fail(BFSX_E_ARG, "persist must be on|off");
         return BFSX_OK;
     }
+    if (k == "vis_front") {
+        if (v == "on") ctx->opt.vis_front = true;
+        else if (v == "off") ctx->opt.vis_front = false;
+        else return fail(BFSX_E_ARG, "vis_front must be on|off");
+        return BFSX_OK;
+    }
     if (k == "persist_front") {
         if (v == "on") ctx->opt.persist_front = true;
         else if (v == "off") ctx->opt.persist_front = false;

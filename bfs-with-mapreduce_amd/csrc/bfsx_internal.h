@@ -39,6 +39,7 @@ struct Options {
     int64_t pull_min_edges = (int64_t)1 << 16; // push -> pull needs at least this many frontier edges (and n/512)
     uint32_t hub_degree = 64;   // degree above which a frontier vertex goes to the multi-workgroup bin
     bool persist = true;        // narrow top-down frontiers run many levels per launch (K3p)
+    bool vis_front = true;      // single device: a pull level after a push / hybrid / K3p level reads vis as its frontier
     bool persist_front = true;  // a BFS's first K3p launch that stops for a pull level also leaves the bitmap frontier
     bool push_log = true;       // single device: per-level push winners go to the push log, not the packed state
     bool hub_lds_skip = true;   // single device: the hub bin skips targets an LDS snapshot of the hubs' visited bits marks

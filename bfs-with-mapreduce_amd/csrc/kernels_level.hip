@@ -630,6 +630,7 @@ int ws_alloc(bfsx_graph *g) {
     BFSX_HIP_TRY(hipMalloc(&ws->par, nv * sizeof(uint32_t)));
     if (g->nranks == 1) BFSX_HIP_TRY(hipMalloc(&ws->pcode, nv));
     BFSX_HIP_TRY(hipMalloc(&ws->vis, ws->nwords * sizeof(u64)));
+    if (g->nranks == 1) BFSX_HIP_TRY(hipMalloc(&ws->vis2, ws->nwords * sizeof(u64))); // option vis_front
     BFSX_HIP_TRY(hipMalloc(&ws->front, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->next, ws->nwords * sizeof(u64)));
     BFSX_HIP_TRY(hipMalloc(&ws->dead, ws->nwords * sizeof(u64)));
@@ -789,7 +790,7 @@ void bfs_workspace_free(BfsWorkspace *ws) {
     for (void *p : {(void *)ws->sendbuf, (void *)ws->recvbuf, (void *)ws->fglob, (void *)ws->persist_seg,
                     (void *)ws->persist_brec, (void *)ws->persist_hseg, ws->persist_ctl})
         if (p) (void)hipFree(p);
-    for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->front, (void *)ws->next,
+    for (void *p : {(void *)ws->st, (void *)ws->off32, (void *)ws->vis, (void *)ws->vis2, (void *)ws->front, (void *)ws->next,
                     (void *)ws->dead, (void *)ws->qa, (void *)ws->qb, (void *)ws->hubs, (void *)ws->top1, (void *)ws->rest,
                     (void *)ws->hub_id, (void *)ws->colh, (void *)ws->hfront, (void *)ws->ring, (void *)ws->d_cursor, (void *)ws->d_red, (void *)ws->remote,
                     (void *)ws->d_dist_ctr, (void *)ws->out64, (void *)ws->rtmp, (void *)ws->pcode, (void *)ws->otop1,
@@ -905,6 +906,8 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
     bool queue_ready = false;
     // the last K3p launch stopped for a pull level and also left its frontier in ws->front (option persist_front)
     bool front_ready = false;
+    // ... and that frontier is vis itself (option vis_front: the launch skipped its queue hand-back, copied nothing)
+    bool front_in_vis = false;
     int td_levels = 0, bu_levels = 0;
     // the bitmap frontier: ws->front after a push -> pull conversion, a pull level's record after a pull level
     const u64 *bmf = ws->front;
@@ -941,18 +944,23 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         // walk their whole hub prefix), the push level ~0.028 ms per million frontier edges (0.72 ms at
         // 17.6 M, 1.74 ms at 67.4 M) -- so hybrid only once the hubs' edges exceed 1.25 U.
         bool hybrid = false, sparse = false;
+        bool vis_front_lvl = false; // this pull level reads vis as its frontier (option vis_front)
         u64 *bu_rec = nullptr; // a pull level's record
         if (dir == BFSX_DIR_TOPDOWN && in_queue && level > 0 && has_hubs(ws) && opt.hybrid != 0 && mfh > 0) {
             const int64_t unv = nv - visited - n_pre;
             hybrid = opt.hybrid == 2 || 100 * mfh > (int64_t)opt.hybrid_pct * unv;
         }
         if (hybrid) {
-            // the hub sweep's frontier: a copy of the visited bitmap (every visited vertex a candidate can touch is
-            // in the frontier: see the pull levels below)
-            BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
+            // the hub sweep's frontier: the visited bitmap (every visited vertex a candidate can touch is in the
+            // frontier: see the pull levels below) -- read in place with vis_front (the sweep writes vis2), else a
+            // copy
+            const bool hv = opt.vis_front && ws->vis2;
+            if (!hv) BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
             u64 *rec = nullptr;
             if (int e = recs.take(&rec)) return e;
-            if (int e = launch_bu_hubonly(g, ws, ws->front, rec, ws->par, level)) return e; // -> rec, vis, par
+            if (hv) ws->bu_vis_out = ws->vis2;
+            if (int e = launch_bu_hubonly(g, ws, hv ? ws->vis : ws->front, rec, ws->par, level)) return e; // -> rec, vis, par
+            if (hv) std::swap(ws->vis, ws->vis2); // the push half claims against the sweep's result
             const Part pt = single_part(g, ws);
             // -> qb; its winners also store their parent in par (they join the record below)
             if (int e = launch_td<false>(g, ws, nf, mf, dmax, level, pt, true, nullptr, 0, ws->par)) return e;
@@ -999,7 +1007,13 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         }
         if (front_ready && dir != BFSX_DIR_BOTTOMUP) // K3p left no queue: its stop test is this switch's
             return fail(BFSX_E_HIP, "internal error: the persistent launch stopped for a pull level the loop did not take");
-        if (dir == BFSX_DIR_BOTTOMUP && in_queue && front_ready) {
+        const bool will_sparse =
+            opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - n_pre) * opt.bu_sparse <= nwords * 64;
+        if (dir == BFSX_DIR_BOTTOMUP && in_queue && front_ready && front_in_vis && !will_sparse) {
+            bmf = ws->vis; // K3p stopped for this pull level without handing its queue back (option vis_front)
+            vis_front_lvl = true;
+            in_queue = false;
+        } else if (dir == BFSX_DIR_BOTTOMUP && in_queue && front_ready && !front_in_vis) {
             bmf = ws->front; // K3p stopped for this pull level and left the frontier in front as well
             in_queue = false;
         } else if (dir == BFSX_DIR_BOTTOMUP && in_queue) {
@@ -1009,8 +1023,16 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             // visited vertices its probes can meet ARE the frontier -- the same hits in the same row order, the
             // same parents and distances -- for one 8-B copy per 64 ids instead of an atomic per frontier vertex
             // (round 6; rounds 1-5 snapshotted the bitmap before a wide push level and XOR-ed it after).
-            BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
-            bmf = ws->front;
+            // Option vis_front (round 6): no copy -- the dense pull kernel reads vis itself as the frontier and
+            // writes vis | its discoveries into vis2 (every word), and the loop swaps the two after the launch.
+            // The sparse kernel updates vis in place, so a sparse level still takes the copy.
+            if (opt.vis_front && ws->vis2 && !will_sparse) {
+                bmf = ws->vis;
+                vis_front_lvl = true;
+            } else {
+                BFSX_HIP_TRY(hipMemcpyAsync(ws->front, ws->vis, nwords * sizeof(u64), hipMemcpyDeviceToDevice, st));
+                bmf = ws->front;
+            }
             in_queue = false;
         } else if (dir == BFSX_DIR_TOPDOWN && !in_queue && queue_ready) {
             // the sparse pull level queued its discoveries (the non-leaves with leaf_skip) itself
@@ -1046,13 +1068,18 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
         nh_found = -1;
         queue_ready = false;
         front_ready = false;
+        front_in_vis = false;
         u64 *plog = nullptr; // this level's push-log segment (a per-level push level with push_log)
         // level 0: a source row longer than persist_dmax enters K3p as its heavy table (row bounds known)
         const bool heavy_src = level == 0 && nf == 1 && dmax > opt.persist_dmax;
         if (dir == BFSX_DIR_TOPDOWN && allow_persist && persist_fits(g, ws, nf, dmax, heavy_src)) {
             // narrow frontier: run as many levels as stay narrow inside one launch (K3p)
             // the BFS's first launch hands a frontier that Beamer sends to a pull level back as the bitmap too
-            u64 *kfront = (level == 0 && opt.direction == BFSX_DIR_AUTO && opt.persist_front) ? ws->front : nullptr;
+            // (with vis_front it is vis itself: the launch only skips handing its queue back, and the pull kernel
+            // reads vis)
+            const bool vf = opt.vis_front && ws->vis2;
+            u64 *kfront = (level == 0 && opt.direction == BFSX_DIR_AUTO && opt.persist_front) ? (vf ? ws->vis : ws->front)
+                                                                                               : nullptr;
             const int ran = heavy_src ? persist_td(g, ws, level, 0, mu, kfront, (uint32_t)source, (uint32_t)dmax,
                                                    src_off[0])
                                       : persist_td(g, ws, level, nf, mu, kfront);
@@ -1086,6 +1113,7 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
                 }
                 std::swap(ws->qa, ws->qb); // K3p hands its last frontier back in qb (and zeroed the ring)
                 front_ready = po.front != 0;
+                front_in_vis = front_ready && kfront == ws->vis;
                 td_levels += ran;
                 level += ran - 1;
                 if (nf == 0) break;
@@ -1104,12 +1132,15 @@ int bfs_run_impl(bfsx_graph *g, int64_t source, bfsx_stats *stats, bool allow_pe
             // few unvisited candidates (the tail levels): the sparse kernel, which also queues its discoveries
             sparse = opt.bu_sparse > 0 && ws->hub_k == 0 && (nv - visited - n_pre) * opt.bu_sparse <= nwords * 64;
             if (int e = recs.take(&bu_rec)) return e;
+            if (vis_front_lvl && sparse) return fail(BFSX_E_HIP, "internal error: a sparse pull level on the visited bitmap");
             if (sparse) {
                 const uint32_t qlim = (uint32_t)(opt.leaf_skip ? std::min<int64_t>(ws->leaf_lo, nv) : nv);
                 if (int e = launch_bu_sparse(g, ws, bmf, bu_rec, ws->par, level, qlim, ws->d_pub, ++ws->pub_seq))
                     return e;
-            } else if (int e = launch_bu<false>(g, ws, bmf, bu_rec, ws->par, level, ws->d_pub, ++ws->pub_seq)) {
-                return e;
+            } else {
+                if (vis_front_lvl) ws->bu_vis_out = ws->vis2;
+                if (int e = launch_bu<false>(g, ws, bmf, bu_rec, ws->par, level, ws->d_pub, ++ws->pub_seq)) return e;
+                if (vis_front_lvl) std::swap(ws->vis, ws->vis2);
             }
             bu_levels++;
         }

@@ -704,13 +704,13 @@ int persist_td(bfsx_graph *g, BfsWorkspace *ws, int level, int64_t nf, int64_t m
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, front, ws->nwords);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, front, front == ws->vis ? (int64_t)0 : ws->nwords);
     else
         hipLaunchKernelGGL(kp64, grid, dim3(kBS), lds, st, g->d_row_off, g->d_col, ws->qa,
                            (uint32_t)nf, ws->persist_seg, ws->persist_brec, ws->qb, ws->vis, ws->st, ws->ring, level,
                            mu, alpha, kPersistLevels, ws->persist_bar, ctl, dout,
                            hub_set(ws), bu_floor(g, ws), opt.persist_abort_at, (u64)opt.persist_dmax,
-                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, front, ws->nwords);
+                           (uint32_t)g->nv, ws->d_err, ws->persist_hseg, h0_v, h0_deg, h0_beg, front, front == ws->vis ? (int64_t)0 : ws->nwords);
     BFSX_LAUNCHED(st);
     BFSX_HIP_TRY(hipEventRecord(ws->ev_level[level], st));
     // spin on workgroup 0's flag; poll the stream now and then so a faulted launch surfaces as an error

@@ -126,7 +126,8 @@ template <class OffT, bool kMf, bool kHubs, int kU, bool kHubOnly, bool kPipe, b
 __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, const uint32_t *__restrict__ col,
                                             const uint32_t *__restrict__ top1, const uint4 *__restrict__ rest,
                                             const u64 *__restrict__ front, u64 *__restrict__ next,
-                                            u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out,
+                                            u64 *__restrict__ vis, u64 *__restrict__ vis_out, u64 *__restrict__ stt,
+                                            uint32_t *__restrict__ par_out,
                                             uint8_t *__restrict__ code_out, LevelSlot *ring, int level,
                                             int64_t nwords, uint32_t fmask, const u64 *__restrict__ hfront,
                                             const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo,
@@ -173,7 +174,10 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = __shfl(incl, 63);
         if (total == 0) { // wave-uniform: every vertex of the group visited or isolated
-            if (wl < nwords) next[wl] = 0ull;
+            if (wl < nwords) {
+                next[wl] = 0ull;
+                if (vis_out) vis_out[wl] = vwl;
+            }
             continue;
         }
         const uint32_t excl = incl - c;
@@ -378,7 +382,10 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
         const u64 nxl = s_nx[wave][lane];
         if (wl < nwords) {
             next[wl] = nxl;
-            if (nxl) vis[wl] = vwl | nxl;
+            // vis_out (the frontier is vis itself): every word goes to the other buffer, vis stays as the level
+            // found it -- another wave may still probe it
+            if (vis_out) vis_out[wl] = vwl | nxl;
+            else if (nxl) vis[wl] = vwl | nxl;
         }
     }
     // claims field: rows walked (phase B)
@@ -389,13 +396,15 @@ __device__ __forceinline__ void k_bu_body(const OffT *__restrict__ row_off, cons
 #define BFSX_K_BU_PARAMS                                                                                        \
     const OffT *__restrict__ row_off, const uint32_t *__restrict__ col, const uint32_t *__restrict__ top1,      \
         const uint4 *__restrict__ rest, const u64 *__restrict__ front, u64 *__restrict__ next,                  \
-        u64 *__restrict__ vis, u64 *__restrict__ stt, uint32_t *__restrict__ par_out, uint8_t *__restrict__ code_out, \
+        u64 *__restrict__ vis, u64 *__restrict__ vis_out, u64 *__restrict__ stt, uint32_t *__restrict__ par_out,       \
+        uint8_t *__restrict__ code_out,                                                                        \
         LevelSlot *ring, int level,                                                                            \
         int64_t nwords, uint32_t fmask,                                                                        \
         const u64 *__restrict__ hfront, const uint32_t *__restrict__ hub_id, uint32_t hub_lim, uint32_t leaf_lo, \
         PrefixSpec pf, Published *pub, u64 seq, uint32_t hub_row_lim
 #define BFSX_K_BU_ARGS                                                                                          \
-    row_off, col, top1, rest, front, next, vis, stt, par_out, code_out, ring, level, nwords, fmask, hfront, hub_id,    \
+    row_off, col, top1, rest, front, next, vis, vis_out, stt, par_out, code_out, ring, level, nwords, fmask, hfront,   \
+        hub_id,                                                                                                \
         hub_lim,                                                                                               \
         leaf_lo, pf,                                                                                           \
         pub, seq, hub_row_lim
@@ -681,7 +690,8 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
 #endif
 #define BFSX_K_BU_LAUNCH(kern)                                                                                   \
     hipLaunchKernelGGL(kern, grid, dim3(kBS), 0, st, row_off, kHubs ? ws->colh : g->d_col, ws->top1, ws->rest, front, \
-                       next, ws->vis, ws->st, par, ws->pcode, ws->ring, level, ws->nwords, ws->top1_flag, ws->hfront,  \
+                       next, ws->vis, ws->bu_vis_out, ws->st, par, ws->pcode, ws->ring, level, ws->nwords,           \
+                       ws->top1_flag, ws->hfront,                                                                       \
                        ws->hub_id,                                                                                      \
                        ws->hub_lim, (uint32_t)std::min<int64_t>(ws->leaf_lo, 0xFFFFFFFFll), lds_prefix<kHubs>(g, ws),  \
                        pub, seq, (uint32_t)std::min<int64_t>(ws->hub_row_lim, 0xFFFFFFFFll))
@@ -691,6 +701,7 @@ int launch_bu_u(bfsx_graph *g, BfsWorkspace *ws, const OffT *row_off, const u64 
 #endif
         BFSX_K_BU_LAUNCH((k_bu<OffT, kMf, kHubs, kU, kHubOnly, kPipe>));
 #undef BFSX_K_BU_LAUNCH
+    ws->bu_vis_out = nullptr; // one-shot
     BFSX_LAUNCHED(st);
     return BFSX_OK;
 }

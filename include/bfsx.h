@@ -116,6 +116,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "offset_bits" = auto|64 (row offsets the traversal kernels read: auto = uint32 when the graph has
  *                 < 2^32 adjacency entries, int64 otherwise; 64 forces int64; fixed at a graph's first BFS)
  *   "persist" = on|off (narrow top-down levels run back to back inside one launch; default on)
+ *   "vis_front" = on|off (one device: the dense pull level after a push, hybrid or K3p level reads the visited
+ *                 bitmap itself as its frontier and writes the updated bitmap into a second buffer, instead of
+ *                 a copy of it; default on)
  *   "persist_front" = on|off (a BFS's first such launch that stops because the next level pulls also leaves its
  *                 last frontier as the pull kernel's bitmap, saving the queue -> bitmap pass; default on)
  *   "push_log" = on|off (one device: a per-level push level writes its winners as (vertex, parent) pairs at
