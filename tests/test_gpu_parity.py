@@ -298,6 +298,51 @@ def test_push_log_matches_state_stores(ctx, persist):
         ctx.set_option("persist", "on")
 
 
+@pytest.mark.parametrize("hybrid", ["auto", "force"])
+def test_vis_front_matches_copy(ctx, hybrid):
+    """Round 6, option vis_front: the dense pull level after a push, hybrid or K3p level reads the visited bitmap
+    itself as its frontier and writes the updated bitmap into a second buffer (the loop swaps the two); off, it
+    reads a copy (K3p's first launch leaves that copy with persist_front, or the loop copies).  Both against the
+    oracle, with identical directions and per-level counts, a valid tree, the device validator and a second read of
+    the result -- on a Kronecker graph (K3p, hub-bin push, pull and sparse pull levels; forced hybrid levels in the
+    second case) and a lollipop (a long path: the K3p launch that stops for a pull comes late)."""
+    cases = []
+    u, v = O.kronecker(14, 16, 11)
+    cases.append((1 << 14, np.asarray(u, np.uint32), np.asarray(v, np.uint32)))
+    plen, leaves = 200, 30000
+    cases.append((plen + leaves,
+                  np.r_[np.arange(plen - 1), np.full(leaves, plen - 1)].astype(np.uint32),
+                  np.r_[np.arange(1, plen), np.arange(plen, plen + leaves)].astype(np.uint32)))
+    try:
+        ctx.set_option("hybrid", hybrid)
+        for nv, u, v in cases:
+            off, col = O.build_sets(nv, u, v)
+            srcs = [int(u[0]), int(v[len(v) // 2]), int(u[-1])]
+            refs = [O.csr_bfs(nv, off, col, s)[0] for s in srcs]
+            levels = {}
+            for mode in ("off", "on"):
+                for pf in ("off", "on"):
+                    ctx.set_option("vis_front", mode)
+                    ctx.set_option("persist_front", pf)
+                    with ctx.from_edges(nv, u, v) as g:
+                        for src, ref in zip(srcs, refs):
+                            d, p, st = g.bfs(src)
+                            assert np.array_equal(d, ref), (mode, pf, src)
+                            assert O.validate(nv, off, col, src, d, p) == 0
+                            assert g.validate()["errors"] == 0
+                            levels[mode, pf, src] = [(l["direction"], l["frontier_in"], l["frontier_out"])
+                                                     for l in g.level_stats(1 << 14)]
+                        d2, _ = g.result()
+                        assert np.array_equal(d2, refs[-1])
+            for src in srcs:
+                assert levels["on", "on", src] == levels["off", "on", src] == levels["off", "off", src] == \
+                    levels["on", "off", src], src
+    finally:
+        ctx.set_option("vis_front", "on")
+        ctx.set_option("persist_front", "on")
+        ctx.set_option("hybrid", "auto")
+
+
 @pytest.mark.parametrize("relabel", ["on", "off"])
 @pytest.mark.parametrize("direction", ["auto", "bottomup"])
 def test_provenance_codes_every_reader(ctx, relabel, direction):
