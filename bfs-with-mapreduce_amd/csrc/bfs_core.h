@@ -869,13 +869,6 @@ __global__ __launch_bounds__(kBS) void k_queue_to_bitmap_dev(const uint32_t *__r
     publish_if_last(cn, pub, seq);
 }
 
-// Frontier of a top-down level as a bitmap without one atomic per vertex: the visited bitmap after
-// the level XOR its snapshot from before the level (bits are only ever set).
-__global__ __launch_bounds__(kBS) void k_new_bits(const u64 *__restrict__ vis, int64_t nwords, u64 *__restrict__ snap) {
-    for (int64_t w = (int64_t)blockIdx.x * kBS + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * kBS)
-        snap[w] ^= vis[w];
-}
-
 // Ballot/popcount compaction of a bitmap into a queue.  A workgroup owns a contiguous range of words
 // (kCompactWords per thread, coalesced), counts its set bits, scans the per-thread counts in LDS and
 // reserves its output range with ONE atomic; the grid is kept small (<= 256 workgroups) so the
