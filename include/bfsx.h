@@ -119,8 +119,9 @@ void bfsx_finalize(bfsx_ctx *ctx);
  *   "vis_front" = on|off (one device: the dense pull level after a push, hybrid or K3p level reads the visited
  *                 bitmap itself as its frontier and writes the updated bitmap into a second buffer, instead of
  *                 a copy of it; default on)
- *   "persist_front" = on|off (a BFS's first such launch that stops because the next level pulls also leaves its
- *                 last frontier as the pull kernel's bitmap, saving the queue -> bitmap pass; default on)
+ *   "persist_front" = on|off (a BFS's first such launch that stops because the next level pulls hands the pull
+ *                 level its frontier bitmap instead of its queue: with vis_front the visited bitmap itself, so the
+ *                 launch only skips its queue hand-back; without, a copy of it in the frontier buffer; default on)
  *   "push_log" = on|off (one device: a per-level push level writes its winners as (vertex, parent) pairs at
  *                 their queue positions instead of scattered state stores; the result read scatters them;
  *                 default on)
